@@ -1,0 +1,162 @@
+/*
+ * pcops.h -- C-ABI of libpcops.so, the MI355X (gfx950) implementation of the
+ * SVDFormer / PointSea per-batch completion hot path.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers (fp32 / int32, C-contiguous) and sizes, no torch
+ *     types; every function launches asynchronously on `stream` (a
+ *     hipStream_t; NULL = the legacy default stream) and never allocates,
+ *     frees or synchronises, so callers may capture it into a hipGraph;
+ *   - outputs are fully written (the reference zero-initialises them in
+ *     C++/Python -- sampling.cpp:25-27, dist_chamfer_3D.py:33-42,56-60 -- so
+ *     "zero + accumulate" outputs are zeroed here with hipMemsetAsync);
+ *   - scratch is caller-provided through `workspace` (size from the matching
+ *     *_workspace_bytes query);
+ *   - the return value is a status code (PCOPS_OK == 0).  The reference
+ *     exits the process (cuda_utils.h:30-39) or prints and returns 0/-1
+ *     (chamfer3D.cu:145-151, emd_cuda.cu:236-249); here nothing exits and
+ *     pcops_status_string() gives the message the Python shim raises.
+ *
+ * Each declaration cites the reference interface it replaces (path:line in
+ * shiyuan0806/SVDFormer_PointSea).
+ */
+#ifndef PCOPS_H_
+#define PCOPS_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *pcops_stream_t; /* == hipStream_t */
+
+enum pcops_status {
+  PCOPS_OK = 0,
+  PCOPS_ERR_INVALID = 1,   /* bad sizes / null pointers */
+  PCOPS_ERR_LAUNCH = 2,    /* hipGetLastError after a launch */
+  PCOPS_ERR_WORKSPACE = 3, /* workspace missing or too small */
+  PCOPS_ERR_UNSUPPORTED = 4
+};
+
+const char *pcops_status_string(int status);
+/* version of the ABI below; bumped on any signature change */
+int pcops_abi_version(void);
+
+/* ---------------- pointnet2_ops (bindings.cpp:6-19) ---------------- */
+
+/* furthest_point_sampling(points, nsamples): sampling.cpp:66-87,
+ * sampling_gpu.cu:69-229.  xyz (B,N,3) -> idx (B,M) int32.
+ * workspace: pcops_fps_workspace_bytes(B,N) bytes (0 when the cloud fits
+ * the register-resident kernel, N <= 16384). */
+unsigned long long pcops_fps_workspace_bytes(int B, int N);
+int pcops_furthest_point_sampling(const float *xyz, int B, int N, int M, int *idx, void *workspace,
+                                  unsigned long long workspace_bytes, pcops_stream_t stream);
+
+/* gather_points(points, idx): sampling.cpp:15-38, sampling_gpu.cu:8-30.
+ * points (B,C,N), idx (B,M) -> out (B,C,M). */
+int pcops_gather_points(const float *points, const int *idx, int B, int C, int N, int M, float *out,
+                        pcops_stream_t stream);
+/* gather_points_grad(grad_out, idx, n): sampling.cpp:40-64, sampling_gpu.cu:34-57.
+ * grad_out (B,C,M) -> grad_points (B,C,N) (overwritten). */
+int pcops_gather_points_grad(const float *grad_out, const int *idx, int B, int C, int N, int M, float *grad_points,
+                             pcops_stream_t stream);
+
+/* group_points(points, idx): group_points.cpp:12-36, group_points_gpu.cu:8-39.
+ * points (B,C,N), idx (B,S,K) -> out (B,C,S,K). */
+int pcops_group_points(const float *points, const int *idx, int B, int C, int N, int S, int K, float *out,
+                       pcops_stream_t stream);
+/* group_points_grad(grad_out, idx, n): group_points.cpp:38-62, group_points_gpu.cu:43-75. */
+int pcops_group_points_grad(const float *grad_out, const int *idx, int B, int C, int N, int S, int K,
+                            float *grad_points, pcops_stream_t stream);
+
+/* ball_query(new_xyz, xyz, radius, nsample): ball_query.cpp:8-32, ball_query_gpu.cu:9-54.
+ * new_xyz (B,M,3), xyz (B,N,3) -> idx (B,M,nsample). */
+int pcops_ball_query(const float *new_xyz, const float *xyz, int B, int N, int M, float radius, int nsample, int *idx,
+                     pcops_stream_t stream);
+
+/* three_nn(unknowns, knows): interpolate.cpp:14-39, interpolate_gpu.cu:9-68.
+ * unknown (B,N,3), known (B,M,3) -> dist2 (B,N,3) squared, idx (B,N,3). */
+int pcops_three_nn(const float *unknown, const float *known, int B, int N, int M, float *dist2, int *idx,
+                   pcops_stream_t stream);
+/* three_interpolate(points, idx, weight): interpolate.cpp:40-68, interpolate_gpu.cu:72-111.
+ * points (B,C,M), idx/weight (B,N,3) -> out (B,C,N). */
+int pcops_three_interpolate(const float *points, const int *idx, const float *weight, int B, int C, int M, int N,
+                            float *out, pcops_stream_t stream);
+/* three_interpolate_grad(grad_out, idx, weight, m): interpolate.cpp:69-99, interpolate_gpu.cu:116-154. */
+int pcops_three_interpolate_grad(const float *grad_out, const int *idx, const float *weight, int B, int C, int N,
+                                 int M, float *grad_points, pcops_stream_t stream);
+
+/* ---------------- kNN (models/model_utils.py:258-286, :807-845) ----------------
+ * query_knn / query_knn_point: K nearest points of p for every query q, in
+ * ascending (squared distance, index) order; distance evaluated exactly as
+ * square_distance's fp32 torch expression.  q (B,S,C), p (B,N,C) channel-last;
+ * pad leading neighbours are skipped (query_knn include_self=False -> 1).
+ * idx (B,S,K) int32; dist (B,S,K) optional (may be NULL).  C <= 512, K+pad <= 64. */
+int pcops_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
+              pcops_stream_t stream);
+
+/* ---------------- Chamfer (metrics/CD/chamfer3D) ----------------
+ * chamfer_3D.forward(xyz1, xyz2, dist1, dist2, idx1, idx2): chamfer_cuda.cpp:17-33,
+ * chamfer3D.cu:12-154. */
+int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B, int N, int M, float *dist1, float *dist2,
+                          int *idx1, int *idx2, pcops_stream_t stream);
+/* chamfer_3D.backward(xyz1, xyz2, gradxyz1, gradxyz2, graddist1, graddist2, idx1, idx2):
+ * chamfer3D.cu:155-195.  gradxyz1/2 are overwritten. */
+int pcops_chamfer_backward(const float *xyz1, const float *xyz2, int B, int N, int M, const float *graddist1,
+                           const float *graddist2, const int *idx1, const int *idx2, float *gradxyz1, float *gradxyz2,
+                           pcops_stream_t stream);
+
+/* ---------------- EMD (metrics/EMD) ----------------
+ * emd.forward(xyz1, xyz2, dist, assignment, price, assignment_inv, bid, bid_increments,
+ *             max_increments, unass_idx, unass_cnt, unass_cnt_sum, cnt_tmp, max_idx, eps, iters):
+ * emd.cpp:14-31, emd_cuda.cu:23-282.  The reference's 12 scratch tensors are
+ * one workspace here.  n must equal m; deterministic auction. */
+unsigned long long pcops_emd_workspace_bytes(int B, int n);
+int pcops_emd_forward(const float *xyz1, const float *xyz2, int B, int n, float eps, int iters, float *dist,
+                      int *assignment, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+/* emd.backward(xyz1, xyz2, gradxyz, graddist, idx): emd_cuda.cu:284-316 (grad for xyz1 only; overwritten). */
+int pcops_emd_backward(const float *xyz1, const float *xyz2, const float *graddist, const int *assignment, int B, int n,
+                       float *gradxyz1, pcops_stream_t stream);
+
+/* ---------------- attention core (nn.MultiheadAttention inside
+ * self_attention / cross_attention, models/model_utils.py:542-617) ----------------
+ * O = softmax(scale * Q K^T) V per (batch*head), flash-style (no L x L
+ * matrix in HBM).  Tensors are addressed as base + bh*s_bh + row*s_row + d
+ * (elements), so the seq-first (L, B*H, hd) layout of MultiheadAttention is
+ * used in place.  dtype 0 = fp32 (f32 MFMA, parity build), 1 = bf16 in/out
+ * with fp32 accumulation.  lse (BH, Lq) fp32 log-sum-exp (natural log) for
+ * the backward.  head_dim in {32, 64, 96, 128}. */
+int pcops_attention_forward(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk,
+                            int D, float scale, int dtype, long long q_sbh, long long q_srow, long long k_sbh,
+                            long long k_srow, long long v_sbh, long long v_srow, long long o_sbh, long long o_srow,
+                            pcops_stream_t stream);
+/* dQ, dK, dV (dtype as forward; dq/dk/dv overwritten).  workspace:
+ * pcops_attention_bwd_workspace_bytes(BH, Lq, Lk, D). */
+unsigned long long pcops_attention_bwd_workspace_bytes(int BH, int Lq, int Lk, int D);
+int pcops_attention_backward(const void *q, const void *k, const void *v, const void *o, const void *dout,
+                             const float *lse, void *dq, void *dk, void *dv, int BH, int Lq, int Lk, int D,
+                             float scale, int dtype, long long q_sbh, long long q_srow, long long k_sbh,
+                             long long k_srow, long long v_sbh, long long v_srow, long long o_sbh, long long o_srow,
+                             void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+
+/* ---------------- depth renderers ----------------
+ * PCViews.get_img (models/model_utils.py:1196-1234 -> points2depth :1080-1115 ->
+ * distribute :1004-1077, size 1): points (B,N,3); rot (V,3,3) row-major =
+ * euler2mat(angle).transpose(1,2); trans (V,3) -> img (B*V, H, W), image
+ * r = b*V + v.  workspace: pcops_points2depth_workspace_bytes. */
+unsigned long long pcops_points2depth_workspace_bytes(int B, int V, int H, int W);
+int pcops_points2depth(const float *points, const float *rot, const float *trans, int B, int N, int V, int H, int W,
+                       float *img, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+/* PCViews_Real.get_img (models_PointSea/mv_utils_zs.py:136-195): points (B,N,3),
+ * rot/rot2 (V,3,3), trans (V,3), kern (3,3) Gaussian (get3DGaussianKernel :197-212)
+ * -> img (B*V, 3, R, R).  grid (B*V, D, R, R) is an output too (the
+ * intermediate voxel grid, [img][z][x][y]). */
+int pcops_points2grid(const float *points, const float *rot, const float *rot2, const float *trans, int B, int N,
+                      int V, int R, int D, float *grid, pcops_stream_t stream);
+int pcops_grid2image(const float *grid, const float *kern, int BV, int D, int R, float *img, void *workspace,
+                     unsigned long long workspace_bytes, pcops_stream_t stream);
+unsigned long long pcops_grid2image_workspace_bytes(int BV, int D, int R);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCOPS_H_ */

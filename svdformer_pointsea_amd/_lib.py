@@ -1,0 +1,127 @@
+"""ctypes binding of libpcops.so (C-ABI: include/pcops.h).
+
+The product path has NO CPU fallback: if the HIP library is missing or a
+tensor is not on the GPU, the call raises.  Tensors are passed as raw device
+pointers; every launch goes to torch's current HIP stream of the tensor's
+device, so the ops compose with torch kernels, streams and hipGraph capture.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libpcops.so")
+
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+F = ctypes.c_float
+LL = ctypes.c_longlong
+ULL = ctypes.c_ulonglong
+
+_SIGS = {
+    "pcops_status_string": (ctypes.c_char_p, [I]),
+    "pcops_abi_version": (I, []),
+    "pcops_fps_workspace_bytes": (ULL, [I, I]),
+    "pcops_furthest_point_sampling": (I, [P, I, I, I, P, P, ULL, P]),
+    "pcops_gather_points": (I, [P, P, I, I, I, I, P, P]),
+    "pcops_gather_points_grad": (I, [P, P, I, I, I, I, P, P]),
+    "pcops_group_points": (I, [P, P, I, I, I, I, I, P, P]),
+    "pcops_group_points_grad": (I, [P, P, I, I, I, I, I, P, P]),
+    "pcops_ball_query": (I, [P, P, I, I, I, F, I, P, P]),
+    "pcops_three_nn": (I, [P, P, I, I, I, P, P, P]),
+    "pcops_three_interpolate": (I, [P, P, P, I, I, I, I, P, P]),
+    "pcops_three_interpolate_grad": (I, [P, P, P, I, I, I, I, P, P]),
+    "pcops_knn": (I, [P, P, I, I, I, I, I, I, P, P, P]),
+    "pcops_chamfer_forward": (I, [P, P, I, I, I, P, P, P, P, P]),
+    "pcops_chamfer_backward": (I, [P, P, I, I, I, P, P, P, P, P, P, P]),
+    "pcops_emd_workspace_bytes": (ULL, [I, I]),
+    "pcops_emd_forward": (I, [P, P, I, I, F, I, P, P, P, ULL, P]),
+    "pcops_emd_backward": (I, [P, P, P, P, I, I, P, P]),
+    "pcops_attention_forward": (I, [P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P]),
+    "pcops_attention_bwd_workspace_bytes": (ULL, [I, I, I, I]),
+    "pcops_attention_backward": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P,
+                                     ULL, P]),
+    "pcops_points2depth_workspace_bytes": (ULL, [I, I, I, I]),
+    "pcops_points2depth": (I, [P, P, P, I, I, I, I, I, P, P, ULL, P]),
+    "pcops_points2grid": (I, [P, P, P, P, I, I, I, I, I, P, P]),
+    "pcops_grid2image_workspace_bytes": (ULL, [I, I, I]),
+    "pcops_grid2image": (I, [P, P, I, I, I, P, P, ULL, P]),
+}
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def lib():
+    """Load libpcops.so once; raise (never fall back) if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"svdformer_pointsea_amd: HIP library not built ({LIB_PATH}); run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)"
+            )
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def check(status, what):
+    if status != 0:
+        msg = lib().pcops_status_string(status).decode()
+        raise RuntimeError(f"{what} failed: {msg} (status {status})")
+
+
+def require_gpu(t, name):
+    """utils.h:5-25 CHECK_CUDA / CHECK_CONTIGUOUS, as RuntimeError."""
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be a contiguous tensor")
+
+
+def require_float(t, name):
+    require_gpu(t, name)
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be a float tensor")
+
+
+def require_int(t, name):
+    require_gpu(t, name)
+    if t.dtype != torch.int32:
+        raise RuntimeError(f"{name} must be an int tensor")
+
+
+class Workspace:
+    """Per-device scratch arena reused across calls (grown, never shrunk).
+
+    Keyed by (device, stream) so concurrent streams never share bytes."""
+
+    _bufs = {}
+
+    @classmethod
+    def get(cls, device, nbytes):
+        if nbytes <= 0:
+            return None
+        key = (device, torch.cuda.current_stream(device).cuda_stream)
+        buf = cls._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+            cls._bufs[key] = buf
+        return buf

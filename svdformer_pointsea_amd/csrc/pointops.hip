@@ -1,0 +1,225 @@
+// group_points, ball_query, three_nn, three_interpolate (+ grads) for gfx950
+// (pointnet2_ops group_points_gpu.cu, ball_query_gpu.cu, interpolate_gpu.cu).
+//
+// The reference launches these with grid = B only (group_points_gpu.cu:34,
+// interpolate_gpu.cu:107) -- B workgroups for the whole chip.  Here every
+// element-wise op is a flat grid-stride launch over all outputs (coalesced
+// writes, >= 256 workgroups), and the search ops map one query per lane.
+#include "common.h"
+
+namespace {
+
+unsigned grid_for(size_t total, int block) {
+  size_t g = (total + block - 1) / block;
+  if (g > 8192) g = 8192;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+// out[b,c,s,k] = points[b,c,idx[b,s,k]]
+__global__ void group_kernel(const float *__restrict__ points, const int *__restrict__ idx, int C, int N, int SK,
+                             size_t total, float *__restrict__ out) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int sk = (int)(e % SK);
+    const size_t bc = e / SK;
+    const size_t b = bc / C;
+    const int a = idx[b * SK + sk];
+    out[e] = ((unsigned)a < (unsigned)N) ? points[bc * N + a] : 0.f;
+  }
+}
+
+__global__ void group_grad_kernel(const float *__restrict__ grad_out, const int *__restrict__ idx, int C, int N,
+                                  int SK, size_t total, float *__restrict__ grad_points) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int sk = (int)(e % SK);
+    const size_t bc = e / SK;
+    const size_t b = bc / C;
+    const int a = idx[b * SK + sk];
+    if ((unsigned)a < (unsigned)N) atomicAdd(grad_points + bc * N + a, grad_out[e]);
+  }
+}
+
+// ball_query_gpu.cu:9-44: first nsample hits in index order; the first hit
+// fills the whole row; no hit leaves zeros.
+__global__ void ball_query_kernel(const float *__restrict__ new_xyz, const float *__restrict__ xyz, int B, int N,
+                                  int M, float r2, int nsample, int *__restrict__ idx) {
+  const size_t tot = (size_t)B * M;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = e / M;
+    const float *p = xyz + b * N * 3;
+    const float nx = new_xyz[e * 3], ny = new_xyz[e * 3 + 1], nz = new_xyz[e * 3 + 2];
+    int *o = idx + e * nsample;
+    int cnt = 0;
+    for (int k = 0; k < N && cnt < nsample; ++k) {
+      const float d2 = sqd3(nx - p[3 * k], ny - p[3 * k + 1], nz - p[3 * k + 2]);
+      if (d2 < r2) {
+        if (cnt == 0)
+          for (int l = 0; l < nsample; ++l) o[l] = k;
+        o[cnt] = k;
+        ++cnt;
+      }
+    }
+    if (cnt == 0)
+      for (int l = 0; l < nsample; ++l) o[l] = 0;
+  }
+}
+
+// interpolate_gpu.cu:9-59 (compare chain in double as the reference; d is fp32)
+__global__ void three_nn_kernel(const float *__restrict__ unknown, const float *__restrict__ known, int B, int N,
+                                int M, float *__restrict__ dist2, int *__restrict__ idx) {
+  extern __shared__ __attribute__((aligned(16))) float4 kt[];
+  constexpr int TN = 1024;
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const float *u = unknown + ((size_t)b * N + (j < N ? j : N - 1)) * 3;
+  const float *kn = known + (size_t)b * M * 3;
+  const float ux = u[0], uy = u[1], uz = u[2];
+  float best1 = INFINITY, best2 = INFINITY, best3 = INFINITY;
+  int bi1 = 0, bi2 = 0, bi3 = 0;
+  for (int t0 = 0; t0 < M; t0 += TN) {
+    const int cnt = min(TN, M - t0);
+    for (int e = threadIdx.x; e < cnt; e += blockDim.x)
+      kt[e] = make_float4(kn[(size_t)(t0 + e) * 3], kn[(size_t)(t0 + e) * 3 + 1], kn[(size_t)(t0 + e) * 3 + 2], 0.f);
+    __syncthreads();
+    for (int e = 0; e < cnt; ++e) {
+      const float4 c = kt[e];
+      const float d = sqd3(ux - c.x, uy - c.y, uz - c.z);
+      const int k = t0 + e;
+      if (d < best1) {
+        best3 = best2; bi3 = bi2;
+        best2 = best1; bi2 = bi1;
+        best1 = d; bi1 = k;
+      } else if (d < best2) {
+        best3 = best2; bi3 = bi2;
+        best2 = d; bi2 = k;
+      } else if (d < best3) {
+        best3 = d; bi3 = k;
+      }
+    }
+    __syncthreads();
+  }
+  if (j < N) {
+    // the reference initialises its bests to 1e40 (double) -> float inf
+    float *dd = dist2 + ((size_t)b * N + j) * 3;
+    int *ii = idx + ((size_t)b * N + j) * 3;
+    dd[0] = best1; dd[1] = best2; dd[2] = best3;
+    ii[0] = bi1; ii[1] = bi2; ii[2] = bi3;
+  }
+}
+
+// interpolate_gpu.cu:72-101: out = p1*w1 + p2*w2 + p3*w3 (contraction order)
+__global__ void three_interp_kernel(const float *__restrict__ points, const int *__restrict__ idx,
+                                    const float *__restrict__ weight, int C, int M, int N, size_t total,
+                                    float *__restrict__ out) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e % N);
+    const size_t bc = e / N;
+    const size_t b = bc / C;
+    const int *ii = idx + (b * N + j) * 3;
+    const float *ww = weight + (b * N + j) * 3;
+    const float *pp = points + bc * M;
+    const int i0 = ii[0], i1 = ii[1], i2 = ii[2];
+    const float p0 = (unsigned)i0 < (unsigned)M ? pp[i0] : 0.f;
+    const float p1 = (unsigned)i1 < (unsigned)M ? pp[i1] : 0.f;
+    const float p2 = (unsigned)i2 < (unsigned)M ? pp[i2] : 0.f;
+    out[e] = __builtin_fmaf(p2, ww[2], __builtin_fmaf(p0, ww[0], p1 * ww[1]));
+  }
+}
+
+__global__ void three_interp_grad_kernel(const float *__restrict__ grad_out, const int *__restrict__ idx,
+                                         const float *__restrict__ weight, int C, int N, int M, size_t total,
+                                         float *__restrict__ grad_points) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e % N);
+    const size_t bc = e / N;
+    const size_t b = bc / C;
+    const int *ii = idx + (b * N + j) * 3;
+    const float *ww = weight + (b * N + j) * 3;
+    const float g = grad_out[e];
+    float *gp = grad_points + bc * M;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      if ((unsigned)ii[r] < (unsigned)M) atomicAdd(gp + ii[r], g * ww[r]);
+  }
+}
+
+}  // namespace
+
+extern "C" int pcops_group_points(const float *points, const int *idx, int B, int C, int N, int S, int K, float *out,
+                                  pcops_stream_t stream) {
+  if (B < 0 || C < 0 || N < 0 || S < 0 || K < 0) return PCOPS_ERR_INVALID;
+  const size_t total = (size_t)B * C * S * K;
+  if (total == 0) return PCOPS_OK;
+  if (!points || !idx || !out) return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(group_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, points, idx, C, N,
+                     S * K, total, out);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_group_points_grad(const float *grad_out, const int *idx, int B, int C, int N, int S, int K,
+                                       float *grad_points, pcops_stream_t stream) {
+  if (B < 0 || C < 0 || N < 0 || S < 0 || K < 0) return PCOPS_ERR_INVALID;
+  if ((size_t)B * C * N == 0) return PCOPS_OK;
+  if (!grad_points) return PCOPS_ERR_INVALID;
+  if (hipMemsetAsync(grad_points, 0, sizeof(float) * (size_t)B * C * N, (hipStream_t)stream) != hipSuccess)
+    return PCOPS_ERR_LAUNCH;
+  const size_t total = (size_t)B * C * S * K;
+  if (total == 0) return PCOPS_OK;
+  if (!grad_out || !idx) return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(group_grad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, grad_out, idx,
+                     C, N, S * K, total, grad_points);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_ball_query(const float *new_xyz, const float *xyz, int B, int N, int M, float radius, int nsample,
+                                int *idx, pcops_stream_t stream) {
+  if (B < 0 || N < 0 || M < 0 || nsample < 0) return PCOPS_ERR_INVALID;
+  const size_t tot = (size_t)B * M;
+  if (tot == 0 || nsample == 0) return PCOPS_OK;
+  if (!new_xyz || !xyz || !idx) return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(ball_query_kernel, dim3(grid_for(tot, 64)), dim3(64), 0, (hipStream_t)stream, new_xyz, xyz, B, N,
+                     M, radius * radius, nsample, idx);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_three_nn(const float *unknown, const float *known, int B, int N, int M, float *dist2, int *idx,
+                              pcops_stream_t stream) {
+  if (B < 0 || N < 0 || M < 0) return PCOPS_ERR_INVALID;
+  if (B == 0 || N == 0) return PCOPS_OK;
+  if (!unknown || !known || !dist2 || !idx) return PCOPS_ERR_INVALID;
+  const dim3 grid((N + 255) / 256, B);
+  hipLaunchKernelGGL(three_nn_kernel, grid, dim3(256), sizeof(float4) * 1024, (hipStream_t)stream, unknown, known, B,
+                     N, M, dist2, idx);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_three_interpolate(const float *points, const int *idx, const float *weight, int B, int C, int M,
+                                       int N, float *out, pcops_stream_t stream) {
+  if (B < 0 || C < 0 || M < 0 || N < 0) return PCOPS_ERR_INVALID;
+  const size_t total = (size_t)B * C * N;
+  if (total == 0) return PCOPS_OK;
+  if (!points || !idx || !weight || !out) return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(three_interp_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, points, idx,
+                     weight, C, M, N, total, out);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_three_interpolate_grad(const float *grad_out, const int *idx, const float *weight, int B, int C,
+                                            int N, int M, float *grad_points, pcops_stream_t stream) {
+  if (B < 0 || C < 0 || M < 0 || N < 0) return PCOPS_ERR_INVALID;
+  if ((size_t)B * C * M == 0) return PCOPS_OK;
+  if (!grad_points) return PCOPS_ERR_INVALID;
+  if (hipMemsetAsync(grad_points, 0, sizeof(float) * (size_t)B * C * M, (hipStream_t)stream) != hipSuccess)
+    return PCOPS_ERR_LAUNCH;
+  const size_t total = (size_t)B * C * N;
+  if (total == 0) return PCOPS_OK;
+  if (!grad_out || !idx || !weight) return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(three_interp_grad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                     grad_out, idx, weight, C, N, M, total, grad_points);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}

@@ -1,0 +1,30 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libpcops.so on cuda:0)")
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+@pytest.fixture(scope="session")
+def dev():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import svdformer_pointsea_amd  # noqa: F401
+
+    svdformer_pointsea_amd.lib()  # raises if the HIP library is missing: never silently skip
+    return torch.device("cuda:0")

@@ -1,0 +1,281 @@
+"""GPU parity: libpcops.so (through the reference-shaped Python API) against
+the CPU oracle and the reference's golden vectors.  Integer/index outputs are
+compared bit-exactly; float outputs with the tolerance stated per test."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def T(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+def _tiled(rng, B, n_unique, N):
+    u = (rng.random((B, n_unique, 3)) - 0.5).astype(np.float32)
+    idx = np.r_[np.arange(n_unique), rng.integers(0, n_unique, N - n_unique)]
+    return np.ascontiguousarray(u[:, idx, :])
+
+
+# ------------------------------------------------------------------ FPS
+FPS_CASES = [
+    ("c1", 4, 2048, 512),
+    ("gt", 2, 16384, 2048),
+    ("n512", 3, 512, 128),
+    ("merge", 2, 2304, 512),
+    ("odd", 2, 513, 100),
+    ("small", 3, 100, 40),
+    ("tiny", 2, 37, 20),
+    ("wave", 1, 64, 64),
+    ("stream", 2, 20000, 300),
+]
+
+
+@pytest.mark.parametrize("name,B,N,M", FPS_CASES)
+def test_fps_bitexact(dev, name, B, N, M):
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
+
+    rng = np.random.default_rng(B * 1000 + N + M)
+    x = (rng.random((B, N, 3)) - 0.5).astype(np.float32)
+    got = furthest_point_sample(T(x, dev), M).cpu().numpy()
+    np.testing.assert_array_equal(got, O.furthest_point_sample(x, M))
+
+
+def test_fps_ties_and_zero_points_bitexact(dev):
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
+
+    rng = np.random.default_rng(1)
+    x = _tiled(rng, 2, 700, 2048)  # PCN-style duplicates, M > unique -> exact ties
+    got = furthest_point_sample(T(x, dev), 1024).cpu().numpy()
+    np.testing.assert_array_equal(got, O.furthest_point_sample(x, 1024))
+    y = (rng.random((2, 2048, 3)) - 0.5).astype(np.float32)
+    y[:, -64:] = 0.0
+    got = furthest_point_sample(T(y, dev), 2000).cpu().numpy()
+    np.testing.assert_array_equal(got, O.furthest_point_sample(y, 2000))
+    z = np.zeros((1, 1024, 3), np.float32)  # nothing valid -> index 0 everywhere
+    assert (furthest_point_sample(T(z, dev), 16).cpu().numpy() == 0).all()
+
+
+def test_fps_full_size_properties(dev):
+    """B=32, 16384 -> 2048 (the loss FPS): size-independent properties."""
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
+
+    g = torch.Generator(device="cpu").manual_seed(2)
+    x = (torch.randn(32, 16384, 3, generator=g) * 0.45).to(dev)
+    idx = furthest_point_sample(x, 2048).long()
+    assert (idx[:, 0] == 0).all()
+    assert all(len(torch.unique(idx[b])) == 2048 for b in range(32))
+    # spot-check two clouds bit-exactly against the oracle
+    for b in (0, 31):
+        np.testing.assert_array_equal(idx[b].cpu().numpy(), O.furthest_point_sample(x[b:b + 1].cpu().numpy(), 2048)[0])
+
+
+# ------------------------------------------------------------------ gather / group
+def test_gather_and_grad(dev):
+    from svdformer_pointsea_amd.pointnet2_utils import gather_operation
+
+    rng = np.random.default_rng(3)
+    f = rng.standard_normal((3, 64, 2048)).astype(np.float32)
+    idx = rng.integers(0, 2048, (3, 512)).astype(np.int32)
+    ft = T(f, dev).requires_grad_(True)
+    out = gather_operation(ft, T(idx, dev))
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), O.gather_operation(f, idx))
+    go = rng.standard_normal(out.shape).astype(np.float32)
+    out.backward(T(go, dev))
+    np.testing.assert_allclose(ft.grad.cpu().numpy(), O.gather_operation_grad(go, idx, 2048), rtol=1e-6, atol=1e-6)
+
+
+def test_group_and_grad(dev):
+    from svdformer_pointsea_amd.pointnet2_utils import grouping_operation
+
+    rng = np.random.default_rng(4)
+    f = rng.standard_normal((2, 128, 512)).astype(np.float32)
+    idx = rng.integers(0, 512, (2, 128, 16)).astype(np.int32)
+    ft = T(f, dev).requires_grad_(True)
+    out = grouping_operation(ft, T(idx, dev))
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), O.grouping_operation(f, idx))
+    go = rng.standard_normal(out.shape).astype(np.float32)
+    out.backward(T(go, dev))
+    # float atomics: order-dependent rounding only
+    np.testing.assert_allclose(ft.grad.cpu().numpy(), O.grouping_operation_grad(go, idx, 512), rtol=1e-5, atol=1e-5)
+
+
+def test_ball_query_bitexact(dev):
+    from svdformer_pointsea_amd.pointnet2_utils import ball_query
+
+    rng = np.random.default_rng(5)
+    xyz = rng.random((2, 1024, 3)).astype(np.float32)
+    new = xyz[:, ::8].copy()
+    new[:, :4] += 5.0  # no neighbours -> zeros
+    for r, ns in [(0.1, 16), (0.2, 32), (0.05, 8)]:
+        got = ball_query(r, ns, T(xyz, dev), T(new, dev)).cpu().numpy()
+        np.testing.assert_array_equal(got, O.ball_query(r, ns, xyz, new))
+
+
+def test_three_nn_and_interpolate(dev):
+    from svdformer_pointsea_amd.pointnet2_utils import three_interpolate, three_nn
+
+    rng = np.random.default_rng(6)
+    unknown = rng.random((2, 2048, 3)).astype(np.float32)
+    known = rng.random((2, 512, 3)).astype(np.float32)
+    dist, idx = three_nn(T(unknown, dev), T(known, dev))
+    odist, oidx, _ = O.three_nn(unknown, known)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oidx)
+    np.testing.assert_array_equal(dist.cpu().numpy(), odist)
+    w = rng.random((2, 2048, 3)).astype(np.float32)
+    f = rng.standard_normal((2, 32, 512)).astype(np.float32)
+    ft = T(f, dev).requires_grad_(True)
+    out = three_interpolate(ft, idx, T(w, dev))
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), O.three_interpolate(f, oidx, w))
+    go = rng.standard_normal(out.shape).astype(np.float32)
+    out.backward(T(go, dev))
+    np.testing.assert_allclose(ft.grad.cpu().numpy(), O.three_interpolate_grad(go, oidx, w, 512), rtol=1e-5,
+                               atol=1e-5)
+
+
+# ------------------------------------------------------------------ Chamfer
+@pytest.mark.parametrize("name", ["c1", "unit", "tiled"])
+def test_chamfer_golden(dev, name):
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    g = golden("chamfer.npz")
+    a, b = g[name + "_a"], g[name + "_b"]
+    d1, d2, i1, i2 = [t.cpu().numpy() for t in chamfer_3DDist()(T(a, dev), T(b, dev))]
+    # the reference's own test criteria (metrics/CD/unit_test.py:22-33)
+    assert ((d1 - g[name + "_d1"]) ** 2).mean() + ((d2 - g[name + "_d2"]) ** 2).mean() < 1e-8
+    np.testing.assert_array_equal(i1, g[name + "_i1"])
+    np.testing.assert_array_equal(i2, g[name + "_i2"])
+    # and bit-exact against the fp32 restatement of chamfer3D.cu
+    od1, od2, oi1, oi2 = O.chamfer_forward(a, b)
+    np.testing.assert_array_equal(d1, od1)
+    np.testing.assert_array_equal(d2, od2)
+    np.testing.assert_array_equal(i1, oi1)
+    np.testing.assert_array_equal(i2, oi2)
+
+
+@pytest.mark.parametrize("B,N,M", [(2, 256, 256), (3, 512, 2048), (2, 2048, 2048), (1, 5000, 3001), (2, 1, 7)])
+def test_chamfer_bitexact_and_backward(dev, B, N, M):
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    rng = np.random.default_rng(N + M)
+    a = (rng.random((B, N, 3)) - 0.5).astype(np.float32)
+    b = (rng.random((B, M, 3)) - 0.5).astype(np.float32)
+    at, bt = T(a, dev).requires_grad_(True), T(b, dev).requires_grad_(True)
+    d1, d2, i1, i2 = chamfer_3DDist()(at, bt)
+    od1, od2, oi1, oi2 = O.chamfer_forward(a, b)
+    np.testing.assert_array_equal(d1.detach().cpu().numpy(), od1)
+    np.testing.assert_array_equal(d2.detach().cpu().numpy(), od2)
+    np.testing.assert_array_equal(i1.cpu().numpy(), oi1)
+    np.testing.assert_array_equal(i2.cpu().numpy(), oi2)
+    w1 = rng.random((B, N)).astype(np.float32)
+    w2 = rng.random((B, M)).astype(np.float32)
+    ((d1 * T(w1, dev)).sum() + (d2 * T(w2, dev)).sum()).backward()
+    g1, g2 = O.chamfer_backward(a, b, w1, w2, oi1, oi2)
+    np.testing.assert_allclose(at.grad.cpu().numpy(), g1, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(bt.grad.cpu().numpy(), g2, rtol=1e-5, atol=1e-6)
+
+
+def test_chamfer_full_size_properties(dev):
+    """B=32, 16384 x 16384 (the loss Chamfer): symmetry and spot checks."""
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    g = torch.Generator(device="cpu").manual_seed(7)
+    a = (torch.randn(32, 16384, 3, generator=g) * 0.45).to(dev)
+    b = (torch.randn(32, 16384, 3, generator=g) * 0.45).to(dev)
+    d1, d2, i1, i2 = chamfer_3DDist()(a, b)
+    e2, e1, j2, j1 = chamfer_3DDist()(b, a)
+    assert torch.equal(d1, e1) and torch.equal(d2, e2) and torch.equal(i1, j1) and torch.equal(i2, j2)
+    # the reported distance is the distance to the reported index
+    nb = torch.gather(b, 1, i1.long().unsqueeze(-1).expand(-1, -1, 3))
+    torch.testing.assert_close(d1, ((a - nb) ** 2).sum(-1), rtol=1e-5, atol=1e-7)
+    for bb in (0, 17):
+        od1, od2, oi1, oi2 = O.chamfer_forward(a[bb:bb + 1, :2048].cpu().numpy(), b[bb:bb + 1].cpu().numpy())
+        s1, s2, si1, si2 = chamfer_3DDist()(a[bb:bb + 1, :2048].contiguous(), b[bb:bb + 1].contiguous())
+        np.testing.assert_array_equal(si1.cpu().numpy(), oi1)
+        np.testing.assert_array_equal(s1.cpu().numpy(), od1)
+
+
+# ------------------------------------------------------------------ kNN
+def test_knn_golden_bitexact(dev):
+    from svdformer_pointsea_amd.model_utils import query_knn, query_knn_point
+
+    k = golden("knn.npz")
+    got = query_knn(16, T(k["qk_xyz"], dev), T(k["qk_new"], dev)).cpu().numpy()
+    np.testing.assert_array_equal(got, k["qk_idx"])
+    got = query_knn(16, T(k["qk_xyz"], dev), T(k["qk_new"], dev), include_self=False).cpu().numpy()
+    np.testing.assert_array_equal(got, k["qk_idx_noself"])
+    for name, K in [("kp3", 16), ("kp64", 8), ("kp256", 4)]:
+        x = T(k[name + "_x"], dev)
+        got = query_knn_point(K, x, x)
+        assert got.dtype == torch.int64
+        np.testing.assert_array_equal(got.cpu().numpy(), k[name + "_idx"])
+
+
+def test_knn_ties_bitexact_vs_oracle(dev):
+    from svdformer_pointsea_amd.model_utils import _knn
+
+    k = golden("knn.npz")
+    idx, d = _knn(T(k["qkt_new"], dev), T(k["qkt_xyz"], dev), 16, want_dist=True)
+    oidx, od = O.knn(k["qkt_new"], k["qkt_xyz"], 16, return_dist=True)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oidx)
+    np.testing.assert_array_equal(d.cpu().numpy(), od)
+    # reference argsort leaves exact ties unordered: the distances per rank agree
+    full = O.square_distance(k["qkt_new"], k["qkt_xyz"])
+    np.testing.assert_array_equal(np.take_along_axis(full, k["qkt_idx"].astype(np.int64), -1), od)
+
+
+def test_group_local_golden(dev):
+    from svdformer_pointsea_amd.model_utils import group_local
+
+    k = golden("knn.npz")
+    x = T(k["kp3_x"], dev).transpose(1, 2).contiguous()
+    g, idx = group_local(x, k=16, return_idx=True)
+    np.testing.assert_array_equal(idx.cpu().numpy(), k["gl_idx"])
+    np.testing.assert_array_equal(g.cpu().numpy(), k["gl_group"])
+
+
+@pytest.mark.parametrize("C,N,K,pad", [(3, 2048, 16, 0), (64, 512, 8, 0), (256, 512, 4, 0), (3, 777, 20, 1),
+                                       (40, 300, 5, 2), (128, 1024, 16, 0)])
+def test_knn_bitexact_vs_oracle(dev, C, N, K, pad):
+    from svdformer_pointsea_amd.model_utils import _knn
+
+    rng = np.random.default_rng(C * N + K)
+    p = rng.standard_normal((2, N, C)).astype(np.float32)
+    q = p[:, : min(N, 300)].copy()
+    idx, d = _knn(T(q, dev), T(p, dev), K, pad, want_dist=True)
+    oidx, od = O.knn(q, p, K, pad, return_dist=True)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oidx)
+    np.testing.assert_array_equal(d.cpu().numpy(), od)
+
+
+def test_fps_subsample_and_sample_and_group(dev):
+    from svdformer_pointsea_amd.model_utils import fps_subsample, sample_and_group_knn
+
+    rng = np.random.default_rng(8)
+    x = (rng.random((2, 2048, 3)) - 0.5).astype(np.float32)
+    sub = fps_subsample(T(x, dev), 512).cpu().numpy()
+    oidx = O.furthest_point_sample(x, 512)
+    np.testing.assert_array_equal(sub, np.take_along_axis(x, oidx[..., None].astype(np.int64), 1))
+    xyz = T(x, dev).transpose(1, 2).contiguous()
+    new_xyz, new_points, idx, grouped = sample_and_group_knn(xyz, xyz, 512, 16)
+    oknn = O.knn(sub, x, 16)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oknn)
+    og = O.grouping_operation(x.transpose(0, 2, 1), oknn) - sub.transpose(0, 2, 1)[..., None]
+    np.testing.assert_array_equal(grouped.cpu().numpy(), og)
+    assert new_points.shape == (2, 6, 512, 16)
+
+
+def test_errors_are_raised_not_exit(dev):
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample, gather_operation
+
+    with pytest.raises(RuntimeError, match="CUDA tensor"):
+        furthest_point_sample(torch.zeros(1, 10, 3), 4)
+    with pytest.raises(RuntimeError, match="int tensor"):
+        gather_operation(torch.zeros(1, 3, 10, device=dev), torch.zeros(1, 4, dtype=torch.int64, device=dev))
+    with pytest.raises(RuntimeError, match="contiguous"):
+        furthest_point_sample(torch.zeros(1, 3, 10, device=dev).transpose(1, 2), 4)
