@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 
 #include "../../include/pcops.h"
 
@@ -39,6 +40,31 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
   return v;
 }
 
+// ---- DPP wave reductions (no LDS traffic; result broadcast via readlane) ----
+// quad_perm [1,0,3,2] / [2,3,0,1], row_half_mirror, row_mirror give every lane
+// its 16-lane row's value; row_bcast15 / row_bcast31 (GFX9 DPP, available on
+// gfx950) fold the four rows into lane 63.
+// `ident` (the op's identity) is the DPP "old" value so LLVM's DPP combiner
+// folds each v_mov_dpp into the following v_max/v_min (one instr per step).
+template <typename Op>
+__device__ __forceinline__ int wave_reduce_i32_dpp(int v, Op op, int ident) {
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0xB1, 0xF, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x4E, 0xF, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x141, 0xF, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x140, 0xF, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x142, 0xA, 0xF, false));
+  v = op(v, __builtin_amdgcn_update_dpp(ident, v, 0x143, 0xC, 0xF, false));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+struct OpMaxI32 {
+  __device__ __forceinline__ int operator()(int a, int b) const { return a > b ? a : b; }
+};
+struct OpMinI32 {
+  __device__ __forceinline__ int operator()(int a, int b) const { return a < b ? a : b; }
+};
+__device__ __forceinline__ int wave_max_i32(int v) { return wave_reduce_i32_dpp(v, OpMaxI32(), INT_MIN); }
+__device__ __forceinline__ int wave_min_i32_dpp(int v) { return wave_reduce_i32_dpp(v, OpMinI32(), INT_MAX); }
+
 // Among the lanes set in `mask`, the one whose lane number has the smallest
 // bit-reversal (prefer bit0 == 0, then bit1 == 0, ...).  Scalar-only work.
 __device__ __forceinline__ int min_bitrev_lane(uint64_t mask) {
@@ -54,6 +80,15 @@ __device__ __forceinline__ int min_bitrev_lane(uint64_t mask) {
 
 __device__ __forceinline__ unsigned bitrev_bits(unsigned v, int bits) {
   return bits == 0 ? 0u : (__builtin_bitreverse32(v) >> (32 - bits));
+}
+
+// Workgroup barrier that only orders LDS: waits for this wave's LDS ops, not
+// for its outstanding global stores (__syncthreads() would also emit
+// s_waitcnt vmcnt(0) and stall on a store's round trip every iteration).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 #define PC_CHECK_LAUNCH()                               \

@@ -12,31 +12,175 @@
 // the argmax and no second barrier or global read is needed.
 // Index parity with sampling_gpu.cu:69-173 is bit-exact (same fused distance,
 // same tie order, same |p|^2 <= 1e-3 skip).
+#include <climits>
 #include <cmath>
 
 #include "common.h"
 
+// Diagnostic build only (tools/fps_probe.hip defines FPS_STAMPS): per-segment
+// s_memtime sums of block 0 / thread 0, never present in libpcops.so.
+#ifdef FPS_STAMPS
+__device__ unsigned long long g_fps_stamps[8];
+__device__ unsigned long long g_fps_wave_stamps[16][4];
+#define FPS_STAMP_DECL unsigned long long _st_prev = __builtin_amdgcn_s_memtime(), _st_acc[4] = {0, 0, 0, 0};
+#define FPS_STAMP(seg)                                          \
+  {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    unsigned long long _n;                                      \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_n)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    _st_acc[seg] += _n - _st_prev;                              \
+    _st_prev = _n;                                              \
+  }
+#define FPS_STAMP_FLUSH \
+  if (blockIdx.x == 0 && threadIdx.x == 0)                      \
+    for (int _s = 0; _s < 4; ++_s) g_fps_stamps[_s] = _st_acc[_s]; \
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0)               \
+    for (int _s = 0; _s < 4; ++_s) g_fps_wave_stamps[threadIdx.x >> 6][_s] = _st_acc[_s];
+#else
+#define FPS_STAMP_DECL
+#define FPS_STAMP(seg)
+#define FPS_STAMP_FLUSH
+#endif
+
 namespace {
 
 constexpr int kFpsThreads = 512;  // == TOTAL_THREADS (cuda_utils.h:13) for N >= 512
-constexpr int kFpsMaxPPT = 32;    // 512 * 32 = 16384 points resident in VGPRs
+constexpr int kFpsMaxPPT = 32;    // 512 * 32 = 16384 points resident in VGPRs (k < 2^14)
 
-// uniform-index register pick: `i` is wave-uniform (readfirstlane), so the
-// switch lowers to scalar branches and the arrays stay in VGPRs.
+// Distances are >= 0 (or the -1 "never" marker), so IEEE fminf/fmaxf and
+// '>' on them equal signed-integer min/max/'>' on their bit patterns; the
+// integer forms need no NaN canonicalisation (v_max x,x,x) in the sweep.
+__device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
+
+// Hardware lane -> reference thread map.  The reference (T threads) breaks
+// ties by the smallest bit-reversed thread id r = rev_L(t), then the smallest
+// k.  Each reference thread's points may be split over SPLIT hardware
+// threads ("halves", SPLIT*PPT points per reference thread).  Hardware
+// thread (w, l) with half h = w / NWT, wv = w % NWT gets the reference thread
+// whose r = l*NWT + wv, so inside a wave the tie-winner is the LOWEST set lane
+// of the ballot (s_ff1), and across waves the order key is r' = r*SPLIT + h.
+// The cross-wave step packs (distance bits, 1023 - r', k) into one 64-bit
+// key and max-reduces the <= 16 per-wave slots with DPP in one row of lanes.
 template <int PPT>
-__device__ __forceinline__ void pick3(const float (&ax)[PPT], const float (&ay)[PPT], const float (&az)[PPT], int i,
-                                      float &x, float &y, float &z) {
-  x = ax[0];
-  y = ay[0];
-  z = az[0];
+__global__ __launch_bounds__(1024) void fps_reg_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
+                                                        int NWT, int SPLIT, int *__restrict__ idx) {
+  const int b = blockIdx.x;
+  const float *p = xyz + (size_t)b * N * 3;
+  int *out = idx + (size_t)b * M;
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  constexpr int kNeverBits = 0xBF800000;  // -1.0f
+  const int half = w / NWT, wv = w - half * NWT;
+  const int rkey = lane * NWT + wv;  // == rev_L(reference thread)
+  const bool active = rkey < T;
+  const int tref = active ? (int)bitrev_bits((unsigned)rkey, L) : 0;
+  const int kbase = tref + T * PPT * half;
+
+  typedef float fvec __attribute__((ext_vector_type(PPT)));
+  typedef int ivec __attribute__((ext_vector_type(PPT)));
+  fvec px, py, pz;
+  ivec tmp;  // running min distance, as float bits
 #pragma unroll
-  for (int c = 1; c < PPT; ++c) {
-    if (i == c) {
-      x = ax[c];
-      y = ay[c];
-      z = az[c];
+  for (int i = 0; i < PPT; ++i) {
+    const int k = kbase + T * i;
+    if (active && k < N) {
+      px[i] = p[3 * k];
+      py[i] = p[3 * k + 1];
+      pz[i] = p[3 * k + 2];
+      const float mag = sqd3(px[i], py[i], pz[i]);
+      tmp[i] = ((double)mag <= 1e-3) ? kNeverBits : fbits(1e10f);  // sampling_gpu.cu:100-101
+    } else {
+      px[i] = py[i] = pz[i] = 0.f;
+      tmp[i] = kNeverBits;
     }
   }
+  // per-wave slots: key (hi, lo) + coords; the leader wave's result
+  __shared__ uint2 skey[16];
+  __shared__ float4 sxyz[16];
+  __shared__ float4 sres;
+  if (t < 16) {
+    skey[t] = make_uint2(0u, 0u);  // absent waves never win
+    sxyz[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+
+  const float x0 = p[0], y0 = p[1], z0 = p[2];
+  float ox = x0, oy = y0, oz = z0;
+  if (t == 0 && M > 0) out[0] = 0;
+  FPS_STAMP_DECL
+  for (int j = 1; j < M; ++j) {
+    // sweep: 8 VALU ops / point, no compare/select chain -- the lane only
+    // tracks its max; the winning slot is recovered once per wave below.
+    int best = kNeverBits;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int d = fbits(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz));
+      tmp[i] = min(d, tmp[i]);
+      best = max(best, tmp[i]);
+    }
+    FPS_STAMP(0)
+    const int wmax = wave_max_i32(best);
+    const uint64_t tied = __ballot(best == wmax);
+    const int wl = (int)__builtin_ctzll(tied);  // lowest lane == smallest r in this wave
+    // first slot of lane wl holding the maximum (in-thread strict '>' rule):
+    // pull lane wl's slots into SGPRs, search on the scalar unit
+    int wbi = PPT - 1;
+#pragma unroll
+    for (int i = PPT - 2; i >= 0; --i) {
+      const int v = __builtin_amdgcn_readlane(tmp[i], wl);
+      wbi = (v == wmax) ? i : wbi;
+    }
+    wbi = __builtin_amdgcn_readfirstlane(wbi);
+    // uniform-index extraction (s_set_gpr_idx / movrel on a register vector)
+    const float cx = px[wbi], cy = py[wbi], cz = pz[wbi];
+    if (lane == wl) {
+      const int r = wl * NWT + wv;
+      const int rp = r * SPLIT + half;
+      const int k = (int)bitrev_bits((unsigned)r, L) + T * (PPT * half + wbi);
+      // lo word: (1023 - r') in [31:18], wave id in [17:14], k in [13:0]
+      skey[w] = make_uint2((unsigned)wmax ^ 0x80000000u,
+                           ((unsigned)(1023 - rp) << 18) | ((unsigned)w << 14) | (unsigned)k);
+      sxyz[w] = make_float4(cx, cy, cz, 0.f);
+    }
+    FPS_STAMP(1)
+    lds_barrier();
+    FPS_STAMP(2)
+    if (w == 0) {  // leader wave: 64-bit max over the <= 16 slots in one DPP row
+      const uint2 kv = skey[lane & 15];
+      const float4 cv = sxyz[lane & 15];
+      unsigned long long key = ((unsigned long long)kv.x << 32) | kv.y;
+#define FPS_DPP_MAX(CTRL)                                                                                   \
+  {                                                                                                        \
+    const unsigned hi = __builtin_amdgcn_update_dpp(0, (int)(key >> 32), CTRL, 0xF, 0xF, false);           \
+    const unsigned lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)key, CTRL, 0xF, 0xF, false);         \
+    const unsigned long long o = ((unsigned long long)hi << 32) | lo;                                      \
+    key = o > key ? o : key;                                                                               \
+  }
+      FPS_DPP_MAX(0xB1)
+      FPS_DPP_MAX(0x4E)
+      FPS_DPP_MAX(0x141)
+      FPS_DPP_MAX(0x140)
+#undef FPS_DPP_MAX
+      const unsigned ghi = __builtin_amdgcn_readfirstlane((unsigned)(key >> 32));
+      const unsigned glo = __builtin_amdgcn_readfirstlane((unsigned)key);
+      if ((int)(ghi ^ 0x80000000u) != kNeverBits) {
+        const int gw = (int)((glo >> 14) & 15u);  // winning wave == its slot lane
+        const int k = (int)(glo & 0x3FFFu);
+        if (lane == gw) sres = make_float4(cv.x, cv.y, cv.z, __int_as_float(k));
+      } else if (lane == 0) {  // no valid point at all: the reference's dists_i[0] == 0
+        sres = make_float4(x0, y0, z0, __int_as_float(0));
+      }
+    }
+    lds_barrier();
+    const float4 rv = sres;
+    ox = rv.x;
+    oy = rv.y;
+    oz = rv.z;
+    if (t == 0) out[j] = __float_as_int(rv.w);
+    FPS_STAMP(3)
+  }
+  FPS_STAMP_FLUSH
 }
 
 struct __align__(16) FpsSlot {
@@ -45,100 +189,6 @@ struct __align__(16) FpsSlot {
   unsigned r;
   int pad0, pad1;
 };
-
-template <int PPT>
-__global__ __launch_bounds__(kFpsThreads) void fps_reg_kernel(const float *__restrict__ xyz, int N, int M, int T,
-                                                               int L, int *__restrict__ idx) {
-  const int b = blockIdx.x;
-  const float *p = xyz + (size_t)b * N * 3;
-  int *out = idx + (size_t)b * M;
-  const int t = threadIdx.x;
-  const int lane = t & 63, w = t >> 6;
-  const int nw = blockDim.x >> 6;
-
-  float px[PPT], py[PPT], pz[PPT], tmp[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + T * i;
-    if (t < T && k < N) {
-      px[i] = p[3 * k];
-      py[i] = p[3 * k + 1];
-      pz[i] = p[3 * k + 2];
-      const float mag = sqd3(px[i], py[i], pz[i]);
-      tmp[i] = ((double)mag <= 1e-3) ? -1.f : 1e10f;  // -1: never selected (sampling_gpu.cu:100-101)
-    } else {
-      px[i] = py[i] = pz[i] = 0.f;
-      tmp[i] = -1.f;
-    }
-  }
-  __shared__ FpsSlot slots[2][kFpsThreads / 64];
-
-  const float x0 = p[0], y0 = p[1], z0 = p[2];
-  float ox = x0, oy = y0, oz = z0;
-  if (t == 0 && M > 0) out[0] = 0;
-  int par = 0;
-  for (int j = 1; j < M; ++j) {
-    float best = -1.f;
-    int bi = 0;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const float d = sqd3(px[i] - ox, py[i] - oy, pz[i] - oz);
-      const float d2 = fminf(d, tmp[i]);
-      tmp[i] = d2;
-      if (d2 > best) {
-        best = d2;
-        bi = i;
-      }
-    }
-    const float wmax = wave_max_f32(best);
-    const uint64_t tied = __ballot(best == wmax);
-    const int wl = min_bitrev_lane(tied);
-    const int wbi = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(bi, wl));
-    float cx, cy, cz;
-    pick3<PPT>(px, py, pz, wbi, cx, cy, cz);
-    cx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), wl));
-    cy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), wl));
-    cz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), wl));
-    if (lane == 0) {
-      const int tw = w * 64 + wl;
-      FpsSlot s;
-      s.d = wmax;
-      s.x = cx;
-      s.y = cy;
-      s.z = cz;
-      s.k = tw + T * wbi;
-      s.r = bitrev_bits((unsigned)tw, L);
-      slots[par][w] = s;
-    }
-    __syncthreads();
-    float gd = slots[par][0].d;
-    int gw = 0;
-    unsigned gr = slots[par][0].r;
-    for (int ww = 1; ww < nw; ++ww) {
-      const float d = slots[par][ww].d;
-      const unsigned r = slots[par][ww].r;
-      if (d > gd || (d == gd && r < gr)) {
-        gd = d;
-        gr = r;
-        gw = ww;
-      }
-    }
-    int k;
-    if (gd > -1.f) {
-      k = slots[par][gw].k;
-      ox = slots[par][gw].x;
-      oy = slots[par][gw].y;
-      oz = slots[par][gw].z;
-    } else {  // no valid point at all: the reference's dists_i[0] == 0
-      k = 0;
-      ox = x0;
-      oy = y0;
-      oz = z0;
-    }
-    if (t == 0) out[j] = k;
-    par ^= 1;
-  }
-}
 
 // Large clouds (N > 16384): same reduction, points streamed from global memory
 // (L2-resident after the first round) and running distances in the workspace.
@@ -176,7 +226,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_stream_kernel(const float *__
         }
       }
     }
-    const float wmax = wave_max_f32(best);
+    const float wmax = __int_as_float(wave_max_i32(fbits(best)));
     const uint64_t tied = __ballot(best == wmax);
     const int wl = min_bitrev_lane(tied);
     const int wk = __builtin_amdgcn_readlane(bk, wl);
@@ -271,21 +321,26 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
   int L = 0;
   while ((1 << L) < T) ++L;
   const int nthreads = T < 64 ? 64 : T;
-  const int ppt = (N + T - 1) / T;
+  const int ppt = (N + T - 1) / T;  // points per reference thread
   hipStream_t s = (hipStream_t)stream;
   if (ppt <= kFpsMaxPPT) {
-#define FPS_CASE(P)                                                                              \
-  if (ppt <= P) {                                                                                \
-    hipLaunchKernelGGL(fps_reg_kernel<P>, dim3(B), dim3(nthreads), 0, s, xyz, N, M, T, L, idx); \
-    PC_CHECK_LAUNCH();                                                                           \
-    return PCOPS_OK;                                                                             \
+    // clouds with > 8 points per reference thread use 2 hardware threads per
+    // reference thread (1024 threads, 4 waves / SIMD) for latency hiding
+    const int split = (ppt > 8 && T == 512) ? 2 : 1;
+    const int per = (ppt + split - 1) / split;
+    const int nwt = nthreads / 64;
+#define FPS_CASE(P)                                                                                       \
+  if (per <= P) {                                                                                         \
+    hipLaunchKernelGGL(fps_reg_kernel<P>, dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt, split, \
+                       idx);                                                                              \
+    PC_CHECK_LAUNCH();                                                                                    \
+    return PCOPS_OK;                                                                                      \
   }
     FPS_CASE(1)
     FPS_CASE(2)
     FPS_CASE(4)
     FPS_CASE(8)
     FPS_CASE(16)
-    FPS_CASE(32)
 #undef FPS_CASE
   }
   if (!workspace || workspace_bytes < pcops_fps_workspace_bytes(B, N)) return PCOPS_ERR_WORKSPACE;
