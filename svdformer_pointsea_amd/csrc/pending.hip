@@ -7,16 +7,6 @@ extern "C" int pcops_emd_forward(const float *, const float *, int, int, float, 
                                  unsigned long long, pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
 extern "C" int pcops_emd_backward(const float *, const float *, const float *, const int *, int, int, float *,
                                   pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
-extern "C" int pcops_attention_forward(const void *, const void *, const void *, void *, float *, int, int, int, int,
-                                       float, int, long long, long long, long long, long long, long long, long long,
-                                       long long, long long, pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
-extern "C" unsigned long long pcops_attention_bwd_workspace_bytes(int, int, int, int) { return 0; }
-extern "C" int pcops_attention_backward(const void *, const void *, const void *, const void *, const void *,
-                                        const float *, void *, void *, void *, int, int, int, int, float, int,
-                                        long long, long long, long long, long long, long long, long long, long long,
-                                        long long, void *, unsigned long long, pcops_stream_t) {
-  return PCOPS_ERR_UNSUPPORTED;
-}
 extern "C" unsigned long long pcops_points2depth_workspace_bytes(int, int, int, int) { return 0; }
 extern "C" int pcops_points2depth(const float *, const float *, const float *, int, int, int, int, int, float *,
                                   void *, unsigned long long, pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
