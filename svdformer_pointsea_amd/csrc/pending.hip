@@ -7,11 +7,3 @@ extern "C" int pcops_emd_forward(const float *, const float *, int, int, float, 
                                  unsigned long long, pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
 extern "C" int pcops_emd_backward(const float *, const float *, const float *, const int *, int, int, float *,
                                   pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
-extern "C" unsigned long long pcops_points2depth_workspace_bytes(int, int, int, int) { return 0; }
-extern "C" int pcops_points2depth(const float *, const float *, const float *, int, int, int, int, int, float *,
-                                  void *, unsigned long long, pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
-extern "C" int pcops_points2grid(const float *, const float *, const float *, const float *, int, int, int, int, int,
-                                 float *, pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }
-extern "C" unsigned long long pcops_grid2image_workspace_bytes(int, int, int) { return 0; }
-extern "C" int pcops_grid2image(const float *, const float *, int, int, int, float *, void *, unsigned long long,
-                                pcops_stream_t) { return PCOPS_ERR_UNSUPPORTED; }

@@ -279,3 +279,44 @@ def test_errors_are_raised_not_exit(dev):
         gather_operation(torch.zeros(1, 3, 10, device=dev), torch.zeros(1, 4, dtype=torch.int64, device=dev))
     with pytest.raises(RuntimeError, match="contiguous"):
         furthest_point_sample(torch.zeros(1, 3, 10, device=dev).transpose(1, 2), 4)
+
+
+# ------------------------------------------------------------------ renderers
+def test_pcviews_depth_golden(dev):
+    from svdformer_pointsea_amd.render import PCViews
+
+    g = golden("depth.npz")
+    view = PCViews(TRANS=-0.7, RESOLUTION=224)
+    np.testing.assert_array_equal(view.rot_mat.numpy(), g["rot"])
+    img = view.get_img(T(g["points"], dev)).cpu().numpy()
+    # same pixels as the reference; values equal up to float-atomic summation order
+    np.testing.assert_array_equal(img != 0, g["img"] != 0)
+    np.testing.assert_allclose(img, g["img"], rtol=1e-6, atol=1e-7)
+
+
+def test_pcviews_depth_vs_oracle_full_batch(dev):
+    from svdformer_pointsea_amd.render import PCViews
+
+    rng = np.random.default_rng(21)
+    pts = (rng.random((32, 2048, 3)) - 0.5).astype(np.float32)
+    pts[:, ::97] = 0.0
+    view = PCViews(TRANS=-0.7, RESOLUTION=224)
+    img = view.get_img(T(pts, dev)).cpu().numpy()
+    ref = O.points2depth(pts, view.rot_mat.numpy(), view.translation.numpy())
+    np.testing.assert_array_equal(img != 0, ref != 0)
+    np.testing.assert_allclose(img, ref, rtol=1e-6, atol=1e-7)
+
+
+def test_pcviews_real_golden(dev):
+    from svdformer_pointsea_amd.render import PCViews_Real
+
+    g = golden("grid.npz")
+    real = PCViews_Real(TRANS=-0.7)
+    np.testing.assert_array_equal(real.rot_mat.numpy(), g["rot"])
+    np.testing.assert_array_equal(real.rot_mat2.numpy(), g["rot2"])
+    np.testing.assert_allclose(real.kernel.numpy(), g["kern"], rtol=0, atol=0)
+    grid = real.points2grid(T(g["points"], dev)).cpu().numpy()
+    np.testing.assert_array_equal(grid, g["grid"])
+    img = real.get_img(T(g["points"], dev)).cpu().numpy()
+    np.testing.assert_allclose(img[:, 0], g["img0"], atol=1e-6)
+    np.testing.assert_array_equal(img[:, 0], img[:, 2])

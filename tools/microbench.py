@@ -39,3 +39,22 @@ print("knn3 32x512x2048 k16 ms", timeit(lambda: _knn(q, small, 16)))
 print("knn3 self 32x2048 k16 ms", timeit(lambda: _knn(small, small, 16)))
 f = torch.randn(32, 512, 64, device=dev)
 print("knn64 self 32x512 k8 ms", timeit(lambda: _knn(f, f, 8)))
+
+from svdformer_pointsea_amd.attention import attention_core  # noqa: E402
+
+for (L, Lk, E, H) in [(2048, 2048, 512, 8), (2048, 2048, 1024, 8), (2048, 512, 512, 8), (512, 512, 768, 8),
+                      (128, 128, 512, 4)]:
+    B = 32
+    q = torch.randn(L, B, E, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(Lk, B, E, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(Lk, B, E, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    fl = 4.0 * B * L * Lk * E
+    ms = timeit(lambda: attention_core(q, k, v, H))
+    o = attention_core(q, k, v, H)
+    g = torch.randn_like(o)
+    msb = timeit(lambda: torch.autograd.grad(o, (q, k, v), g, retain_graph=True))
+    print(f"attn bf16 L{L}xLk{Lk} E{E} H{H}: fwd {ms:.3f} ms {fl / ms / 1e9:.1f} TF/s; bwd {msb:.3f} ms "
+          f"{2.5 * fl / msb / 1e9:.1f} TF/s")
+    qf, kf, vf = q.float().detach(), k.float().detach(), v.float().detach()
+    msf = timeit(lambda: attention_core(qf, kf, vf, H), iters=2, warm=1)
+    print(f"   fp32 fwd {msf:.3f} ms {fl / msf / 1e9:.1f} TF/s")
