@@ -138,6 +138,23 @@ int pcops_attention_backward(const void *q, const void *k, const void *v, const 
                              long long k_srow, long long v_sbh, long long v_srow, long long o_sbh, long long o_srow,
                              void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 
+/* The three launches of pcops_attention_backward, exposed separately so a
+ * caller can time or overlap them: delta = rowsum(dO o O) into workspace,
+ * then dQ (query-on-lane pass), then dK/dV (key-on-lane pass). */
+int pcops_attention_bwd_preprocess(const void *o, const void *dout, int BH, int Lq, int D, int dtype, long long o_sbh,
+                                   long long o_srow, void *workspace, unsigned long long workspace_bytes,
+                                   pcops_stream_t stream);
+int pcops_attention_bwd_dq(const void *q, const void *k, const void *v, const void *dout, const float *lse,
+                           void *dq, int BH, int Lq, int Lk, int D, float scale, int dtype, long long q_sbh,
+                           long long q_srow, long long k_sbh, long long k_srow, long long v_sbh, long long v_srow,
+                           long long o_sbh, long long o_srow, const void *workspace, unsigned long long workspace_bytes,
+                           pcops_stream_t stream);
+int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const void *dout, const float *lse,
+                            void *dk, void *dv, int BH, int Lq, int Lk, int D, float scale, int dtype,
+                            long long q_sbh, long long q_srow, long long k_sbh, long long k_srow, long long v_sbh,
+                            long long v_srow, long long o_sbh, long long o_srow, const void *workspace,
+                            unsigned long long workspace_bytes, pcops_stream_t stream);
+
 /* ---------------- depth renderers ----------------
  * PCViews.get_img (models/model_utils.py:1196-1234 -> points2depth :1080-1115 ->
  * distribute :1004-1077, size 1): points (B,N,3); rot (V,3,3) row-major =

@@ -44,6 +44,10 @@ _SIGS = {
     "pcops_attention_bwd_workspace_bytes": (ULL, [I, I, I, I]),
     "pcops_attention_backward": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P,
                                      ULL, P]),
+    "pcops_attention_bwd_preprocess": (I, [P, P, I, I, I, I, LL, LL, P, ULL, P]),
+    "pcops_attention_bwd_dq": (I, [P, P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
+    "pcops_attention_bwd_dkv": (I, [P, P, P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL,
+                                    P]),
     "pcops_points2depth_workspace_bytes": (ULL, [I, I, I, I]),
     "pcops_points2depth": (I, [P, P, P, I, I, I, I, I, P, P, ULL, P]),
     "pcops_points2grid": (I, [P, P, P, P, I, I, I, I, I, P, P]),
@@ -86,6 +90,52 @@ def check(status, what):
     if status != 0:
         msg = lib().pcops_status_string(status).decode()
         raise RuntimeError(f"{what} failed: {msg} (status {status})")
+
+
+class KernelTimer:
+    """Opt-in HIP-event timing of every C-ABI launch, per call name.
+
+    Events are recorded on the very stream the call launches on (torch's
+    current stream of the current device), so spans are exact per call even
+    when the caller uses side streams.  Used by bench.py; off by default."""
+
+    spans = None  # name -> [(start_event, end_event)] while enabled
+
+    @classmethod
+    def enable(cls):
+        cls.spans = {}
+
+    @classmethod
+    def disable(cls):
+        cls.spans = None
+
+    @classmethod
+    def reset(cls):
+        if cls.spans is not None:
+            cls.spans = {}
+
+    @classmethod
+    def summary(cls):
+        """name -> (launches, mean ms, total ms); call after synchronising."""
+        out = {}
+        for name, evs in (cls.spans or {}).items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            out[name] = (len(ms), sum(ms) / len(ms), sum(ms))
+        return out
+
+
+def call(what, fn, *args):
+    """Run one C-ABI entry point on the current device; raise on failure."""
+    spans = KernelTimer.spans
+    if spans is None:
+        return check(fn(*args), what)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    status = fn(*args)
+    e1.record(s)
+    spans.setdefault(what, []).append((e0, e1))
+    check(status, what)
 
 
 def require_gpu(t, name):

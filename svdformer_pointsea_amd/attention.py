@@ -19,7 +19,7 @@ from torch import nn
 from torch.autograd import Function
 
 from . import _lib
-from ._lib import check, lib, ptr, stream_of
+from ._lib import call, lib, ptr, stream_of
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
@@ -48,9 +48,8 @@ class AttentionCore(Function):
         sq, rq = _strides(q, heads)
         sk, rk = _strides(k, heads)
         with torch.cuda.device(q.device):
-            check(lib().pcops_attention_forward(ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B * heads, Lq, Lk, hd,
-                                                float(scale), _DT[q.dtype], sq, rq, sk, rk, sk, rk, sq, rq,
-                                                stream_of(q)), "attention forward")
+            call("attention forward", lib().pcops_attention_forward, ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse),
+                 B * heads, Lq, Lk, hd, float(scale), _DT[q.dtype], sq, rq, sk, rk, sk, rk, sq, rq, stream_of(q))
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.heads, ctx.scale = heads, scale
         return o
@@ -68,11 +67,16 @@ class AttentionCore(Function):
         sk, rk = _strides(k, heads)
         wsb = lib().pcops_attention_bwd_workspace_bytes(B * heads, Lq, Lk, hd)
         ws = _lib.Workspace.get(q.device, wsb)
+        BH, dt = B * heads, _DT[q.dtype]
+        st = (sq, rq, sk, rk, sk, rk, sq, rq)
         with torch.cuda.device(q.device):
-            check(lib().pcops_attention_backward(ptr(q), ptr(k), ptr(v), ptr(o), ptr(do), ptr(lse), ptr(dq), ptr(dk),
-                                                 ptr(dv), B * heads, Lq, Lk, hd, float(scale), _DT[q.dtype], sq, rq,
-                                                 sk, rk, sk, rk, sq, rq, ptr(ws), wsb, stream_of(q)),
-                  "attention backward")
+            stream = stream_of(q)
+            call("attention bwd delta", lib().pcops_attention_bwd_preprocess, ptr(o), ptr(do), BH, Lq, hd, dt, sq, rq,
+                 ptr(ws), wsb, stream)
+            call("attention bwd dq", lib().pcops_attention_bwd_dq, ptr(q), ptr(k), ptr(v), ptr(do), ptr(lse), ptr(dq),
+                 BH, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream)
+            call("attention bwd dkv", lib().pcops_attention_bwd_dkv, ptr(q), ptr(k), ptr(v), ptr(do), ptr(lse), ptr(dk),
+                 ptr(dv), BH, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream)
         return dq, dk, dv, None, None
 
 

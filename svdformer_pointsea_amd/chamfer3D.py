@@ -9,12 +9,14 @@ inputs' device and the kernels run on torch's current stream.
 import torch
 from torch import nn
 from torch.autograd import Function
+from torch.amp import custom_bwd, custom_fwd
 
-from ._lib import check, lib, ptr, require_float, stream_of
+from ._lib import call, lib, ptr, require_float, stream_of
 
 
 class chamfer_3DFunction(Function):
     @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, xyz1, xyz2):
         require_float(xyz1, "xyz1")
         require_float(xyz2, "xyz2")
@@ -26,13 +28,14 @@ class chamfer_3DFunction(Function):
         idx1 = torch.empty(B, n, dtype=torch.int32, device=dev)
         idx2 = torch.empty(B, m, dtype=torch.int32, device=dev)
         with torch.cuda.device(dev):
-            check(lib().pcops_chamfer_forward(ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist1), ptr(dist2), ptr(idx1),
-                                              ptr(idx2), stream_of(xyz1)), "chamfer_3D.forward")
+            call("chamfer_3D.forward", lib().pcops_chamfer_forward, ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist1),
+                 ptr(dist2), ptr(idx1), ptr(idx2), stream_of(xyz1))
         ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
         ctx.mark_non_differentiable(idx1, idx2)
         return dist1, dist2, idx1, idx2
 
     @staticmethod
+    @custom_bwd(device_type="cuda")
     def backward(ctx, graddist1, graddist2, gradidx1, gradidx2):
         xyz1, xyz2, idx1, idx2 = ctx.saved_tensors
         B, n, _ = xyz1.shape
@@ -43,9 +46,8 @@ class chamfer_3DFunction(Function):
         g1 = torch.empty(B, n, 3, device=dev)
         g2 = torch.empty(B, m, 3, device=dev)
         with torch.cuda.device(dev):
-            check(lib().pcops_chamfer_backward(ptr(xyz1), ptr(xyz2), B, n, m, ptr(graddist1), ptr(graddist2),
-                                               ptr(idx1), ptr(idx2), ptr(g1), ptr(g2), stream_of(xyz1)),
-                  "chamfer_3D.backward")
+            call("chamfer_3D.backward", lib().pcops_chamfer_backward, ptr(xyz1), ptr(xyz2), B, n, m, ptr(graddist1),
+                 ptr(graddist2), ptr(idx1), ptr(idx2), ptr(g1), ptr(g2), stream_of(xyz1))
         return g1, g2
 
 

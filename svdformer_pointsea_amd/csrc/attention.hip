@@ -70,7 +70,9 @@ struct Prec<__bf16, D> {
   }
   // Y[db] += Rows^T . X   (X fp32 accumulator, converted to bf16 in place)
   __device__ static void product2(f32x16 (&Y)[D / 32], const __bf16 *lds, const f32x16 &X) {
+#if defined(__HIP_DEVICE_COMPILE__)
     const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+    typedef __attribute__((address_space(3))) short4v lds_s4;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 b;
@@ -80,17 +82,14 @@ struct Prec<__bf16, D> {
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) {
         const int col = db * 32 + 16 * g + 4 * p;
-        bf16x8 a;
-#if defined(__HIP_DEVICE_COMPILE__)
-        typedef __attribute__((address_space(3))) short4v lds_s4;
         const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + row0 * kStride + col));
         const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + (row0 + 8) * kStride + col));
-        a = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1, 2, 3, 4, 5,
-                                    6, 7);
-#endif
+        const bf16x8 a = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1,
+                                                 2, 3, 4, 5, 6, 7);
         Y[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, Y[db], 0, 0, 0);
       }
     }
+#endif
   }
   __device__ static float to_f(__bf16 v) { return (float)v; }
   __device__ static __bf16 from_f(float v) { return (__bf16)v; }
@@ -386,35 +385,62 @@ int launch_fwd(const void *q, const void *k, const void *v, void *o, float *lse,
 }
 
 template <typename T>
-int launch_bwd(const void *q, const void *k, const void *v, const void *o, const void *dout, const float *lse,
-               void *dq, void *dk, void *dv, float *delta, int BH, int Lq, int Lk, int D, float scale,
-               const Strides &st, hipStream_t s) {
-  {
-    const int rows = BH * Lq;
-    hipLaunchKernelGGL((attn_delta_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0, s, (const T *)o, (const T *)dout,
-                       delta, BH, Lq, D, st);
-    PC_CHECK_LAUNCH();
-  }
+int launch_delta(const void *o, const void *dout, float *delta, int BH, int Lq, int D, const Strides &st,
+                 hipStream_t s) {
+  const int rows = BH * Lq;
+  hipLaunchKernelGGL((attn_delta_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0, s, (const T *)o, (const T *)dout,
+                     delta, BH, Lq, D, st);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+template <typename T>
+int launch_dq(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+              void *dq, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s) {
   const dim3 gq((Lq + kWaves * 32 - 1) / (kWaves * 32), BH);
-  const dim3 gk((Lk + kWaves * 32 - 1) / (kWaves * 32), BH);
-#define ATT_BWD(DD)                                                                                              \
-  case DD:                                                                                                       \
-    hipLaunchKernelGGL((attn_dq_kernel<T, DD>), gq, dim3(kThreads), 0, s, (const T *)q, (const T *)k,            \
-                       (const T *)v, (const T *)dout, lse, delta, (T *)dq, Lq, Lk, scale, st);                   \
-    PC_CHECK_LAUNCH();                                                                                           \
-    hipLaunchKernelGGL((attn_dkv_kernel<T, DD>), gk, dim3(kThreads), 0, s, (const T *)q, (const T *)k,           \
-                       (const T *)v, (const T *)dout, lse, delta, (T *)dk, (T *)dv, Lq, Lk, scale, st);          \
-    PC_CHECK_LAUNCH();                                                                                           \
+#define ATT_DQ(DD)                                                                                              \
+  case DD:                                                                                                      \
+    hipLaunchKernelGGL((attn_dq_kernel<T, DD>), gq, dim3(kThreads), 0, s, (const T *)q, (const T *)k,           \
+                       (const T *)v, (const T *)dout, lse, delta, (T *)dq, Lq, Lk, scale, st);                  \
     break;
   switch (D) {
-    ATT_BWD(32)
-    ATT_BWD(64)
-    ATT_BWD(96)
-    ATT_BWD(128)
+    ATT_DQ(32)
+    ATT_DQ(64)
+    ATT_DQ(96)
+    ATT_DQ(128)
     default:
       return PCOPS_ERR_UNSUPPORTED;
   }
-#undef ATT_BWD
+#undef ATT_DQ
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+template <typename T>
+int launch_dkv(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+               void *dk, void *dv, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s) {
+  const dim3 gk((Lk + kWaves * 32 - 1) / (kWaves * 32), BH);
+#define ATT_DKV(DD)                                                                                             \
+  case DD:                                                                                                      \
+    hipLaunchKernelGGL((attn_dkv_kernel<T, DD>), gk, dim3(kThreads), 0, s, (const T *)q, (const T *)k,          \
+                       (const T *)v, (const T *)dout, lse, delta, (T *)dk, (T *)dv, Lq, Lk, scale, st);         \
+    break;
+  switch (D) {
+    ATT_DKV(32)
+    ATT_DKV(64)
+    ATT_DKV(96)
+    ATT_DKV(128)
+    default:
+      return PCOPS_ERR_UNSUPPORTED;
+  }
+#undef ATT_DKV
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+int check_common(int BH, int Lq, int Lk, int D, int dtype) {
+  if (BH < 0 || Lq < 0 || Lk < 0) return PCOPS_ERR_INVALID;
+  if (D % 32 != 0 || D <= 0 || D > 128 || (dtype != 0 && dtype != 1)) return PCOPS_ERR_UNSUPPORTED;
   return PCOPS_OK;
 }
 
@@ -445,6 +471,64 @@ extern "C" unsigned long long pcops_attention_bwd_workspace_bytes(int BH, int Lq
   return (unsigned long long)BH * Lq * sizeof(float);
 }
 
+extern "C" int pcops_attention_bwd_preprocess(const void *o, const void *dout, int BH, int Lq, int D, int dtype,
+                                              long long o_sbh, long long o_srow, void *workspace,
+                                              unsigned long long workspace_bytes, pcops_stream_t stream) {
+  int rc = check_common(BH, Lq, 1, D, dtype);
+  if (rc) return rc;
+  if (BH == 0 || Lq == 0) return PCOPS_OK;
+  if (!o || !dout) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(BH, Lq, 1, D)) return PCOPS_ERR_WORKSPACE;
+  const Strides st{0, 0, 0, 0, 0, 0, o_sbh, o_srow};
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == 0 ? launch_delta<float>(o, dout, (float *)workspace, BH, Lq, D, st, s)
+                    : launch_delta<__bf16>(o, dout, (float *)workspace, BH, Lq, D, st, s);
+}
+
+extern "C" int pcops_attention_bwd_dq(const void *q, const void *k, const void *v, const void *dout, const float *lse,
+                                      void *dq, int BH, int Lq, int Lk, int D, float scale, int dtype,
+                                      long long q_sbh, long long q_srow, long long k_sbh, long long k_srow,
+                                      long long v_sbh, long long v_srow, long long o_sbh, long long o_srow,
+                                      const void *workspace, unsigned long long workspace_bytes,
+                                      pcops_stream_t stream) {
+  int rc = check_common(BH, Lq, Lk, D, dtype);
+  if (rc) return rc;
+  if (BH == 0 || Lq == 0) return PCOPS_OK;
+  if (!q || !k || !v || !dout || !lse || !dq || Lk <= 0) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(BH, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
+  const int es = dtype == 0 ? 4 : 2;
+  if (!aligned_ok(q, q_sbh, q_srow, es) || !aligned_ok(k, k_sbh, k_srow, es) || !aligned_ok(v, v_sbh, v_srow, es) ||
+      !aligned_ok(dout, o_sbh, o_srow, es) || !aligned_ok(dq, q_sbh, q_srow, es))
+    return PCOPS_ERR_UNSUPPORTED;
+  const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
+  hipStream_t s = (hipStream_t)stream;
+  const float *delta = (const float *)workspace;
+  return dtype == 0 ? launch_dq<float>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s)
+                    : launch_dq<__bf16>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s);
+}
+
+extern "C" int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const void *dout,
+                                       const float *lse, void *dk, void *dv, int BH, int Lq, int Lk, int D,
+                                       float scale, int dtype, long long q_sbh, long long q_srow, long long k_sbh,
+                                       long long k_srow, long long v_sbh, long long v_srow, long long o_sbh,
+                                       long long o_srow, const void *workspace, unsigned long long workspace_bytes,
+                                       pcops_stream_t stream) {
+  int rc = check_common(BH, Lq, Lk, D, dtype);
+  if (rc) return rc;
+  if (BH == 0 || Lk == 0) return PCOPS_OK;
+  if (!q || !k || !v || !dout || !lse || !dk || !dv || Lq <= 0) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(BH, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
+  const int es = dtype == 0 ? 4 : 2;
+  if (!aligned_ok(q, q_sbh, q_srow, es) || !aligned_ok(k, k_sbh, k_srow, es) || !aligned_ok(v, v_sbh, v_srow, es) ||
+      !aligned_ok(dout, o_sbh, o_srow, es) || !aligned_ok(dk, k_sbh, k_srow, es) || !aligned_ok(dv, v_sbh, v_srow, es))
+    return PCOPS_ERR_UNSUPPORTED;
+  const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
+  hipStream_t s = (hipStream_t)stream;
+  const float *delta = (const float *)workspace;
+  return dtype == 0 ? launch_dkv<float>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s)
+                    : launch_dkv<__bf16>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
+}
+
 // dq/dk/dv use the q/k/v strides; dout uses the o strides.
 extern "C" int pcops_attention_backward(const void *q, const void *k, const void *v, const void *o, const void *dout,
                                         const float *lse, void *dq, void *dk, void *dv, int BH, int Lq, int Lk, int D,
@@ -452,20 +536,14 @@ extern "C" int pcops_attention_backward(const void *q, const void *k, const void
                                         long long k_srow, long long v_sbh, long long v_srow, long long o_sbh,
                                         long long o_srow, void *workspace, unsigned long long workspace_bytes,
                                         pcops_stream_t stream) {
-  if (BH < 0 || Lq < 0 || Lk < 0) return PCOPS_ERR_INVALID;
-  if (BH == 0 || Lq == 0 || Lk == 0) return PCOPS_OK;
-  if (!q || !k || !v || !o || !dout || !lse || !dq || !dk || !dv) return PCOPS_ERR_INVALID;
-  if (D % 32 != 0 || D > 128 || (dtype != 0 && dtype != 1)) return PCOPS_ERR_UNSUPPORTED;
-  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(BH, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
+  if (BH == 0 || Lq == 0 || Lk == 0) return check_common(BH, Lq, Lk, D, dtype);
   const int es = dtype == 0 ? 4 : 2;
-  if (!aligned_ok(q, q_sbh, q_srow, es) || !aligned_ok(k, k_sbh, k_srow, es) || !aligned_ok(v, v_sbh, v_srow, es) ||
-      !aligned_ok(o, o_sbh, o_srow, es) || !aligned_ok(dout, o_sbh, o_srow, es) || !aligned_ok(dq, q_sbh, q_srow, es) ||
-      !aligned_ok(dk, k_sbh, k_srow, es) || !aligned_ok(dv, v_sbh, v_srow, es))
-    return PCOPS_ERR_UNSUPPORTED;
-  const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
-  hipStream_t s = (hipStream_t)stream;
-  return dtype == 0 ? launch_bwd<float>(q, k, v, o, dout, lse, dq, dk, dv, (float *)workspace, BH, Lq, Lk, D, scale,
-                                        st, s)
-                    : launch_bwd<__bf16>(q, k, v, o, dout, lse, dq, dk, dv, (float *)workspace, BH, Lq, Lk, D, scale,
-                                         st, s);
+  if (o && !aligned_ok(o, o_sbh, o_srow, es)) return PCOPS_ERR_UNSUPPORTED;
+  int rc = pcops_attention_bwd_preprocess(o, dout, BH, Lq, D, dtype, o_sbh, o_srow, workspace, workspace_bytes, stream);
+  if (rc) return rc;
+  rc = pcops_attention_bwd_dq(q, k, v, dout, lse, dq, BH, Lq, Lk, D, scale, dtype, q_sbh, q_srow, k_sbh, k_srow, v_sbh,
+                              v_srow, o_sbh, o_srow, workspace, workspace_bytes, stream);
+  if (rc) return rc;
+  return pcops_attention_bwd_dkv(q, k, v, dout, lse, dk, dv, BH, Lq, Lk, D, scale, dtype, q_sbh, q_srow, k_sbh, k_srow,
+                                 v_sbh, v_srow, o_sbh, o_srow, workspace, workspace_bytes, stream);
 }

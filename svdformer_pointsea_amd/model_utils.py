@@ -16,14 +16,14 @@ import numpy as np
 import torch
 from torch import nn
 
-from ._lib import check, lib, ptr, require_float, stream_of
+from ._lib import call, lib, ptr, require_float, stream_of
 from .pointnet2_utils import furthest_point_sample, gather_operation, grouping_operation
 
 
 def _knn(q, p, k, pad=0, want_dist=False):
     """K nearest of p for every row of q; q (B,S,C), p (B,N,C) fp32 on the GPU."""
-    q = q.contiguous()
-    p = p.contiguous()
+    q = q.float().contiguous()  # distances are evaluated in fp32 (also under autocast)
+    p = p.float().contiguous()
     require_float(q, "new_xyz")
     require_float(p, "xyz")
     B, S, C = q.shape
@@ -35,7 +35,7 @@ def _knn(q, p, k, pad=0, want_dist=False):
     idx = torch.empty(B, S, k, dtype=torch.int32, device=q.device)
     dist = torch.empty(B, S, k, dtype=torch.float32, device=q.device) if want_dist else None
     with torch.cuda.device(q.device):
-        check(lib().pcops_knn(ptr(q), ptr(p), B, S, N, C, k, pad, ptr(idx), ptr(dist), stream_of(q)), "knn")
+        call("knn", lib().pcops_knn, ptr(q), ptr(p), B, S, N, C, k, pad, ptr(idx), ptr(dist), stream_of(q))
     return (idx, dist) if want_dist else idx
 
 

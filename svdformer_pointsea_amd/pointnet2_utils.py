@@ -13,13 +13,15 @@ pointnet2_ops_lib/pointnet2_ops/pointnet2_utils.py:34-379:
 import torch
 import torch.nn as nn
 from torch.autograd import Function
+from torch.amp import custom_bwd, custom_fwd
 
 from . import _lib
-from ._lib import check, lib, ptr, require_float, require_int, stream_of
+from ._lib import call, lib, ptr, require_float, require_int, stream_of
 
 
 class FurthestPointSampling(Function):
     @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, xyz, npoint):
         require_float(xyz, "points")
         B, N, _ = xyz.shape
@@ -28,12 +30,13 @@ class FurthestPointSampling(Function):
         wsb = lib().pcops_fps_workspace_bytes(B, N)
         ws = _lib.Workspace.get(xyz.device, wsb)
         with torch.cuda.device(xyz.device):
-            check(lib().pcops_furthest_point_sampling(ptr(xyz), B, N, npoint, ptr(out), ptr(ws), wsb, stream_of(xyz)),
-                  "furthest_point_sampling")
+            call("furthest_point_sampling", lib().pcops_furthest_point_sampling, ptr(xyz), B, N, npoint, ptr(out),
+                 ptr(ws), wsb, stream_of(xyz))
         ctx.mark_non_differentiable(out)
         return out
 
     @staticmethod
+    @custom_bwd(device_type="cuda")
     def backward(ctx, grad_out):
         return ()
 
@@ -43,6 +46,7 @@ furthest_point_sample = FurthestPointSampling.apply
 
 class GatherOperation(Function):
     @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, features, idx):
         require_float(features, "points")
         require_int(idx, "idx")
@@ -50,12 +54,13 @@ class GatherOperation(Function):
         M = idx.shape[1]
         out = torch.empty(B, C, M, dtype=torch.float32, device=features.device)
         with torch.cuda.device(features.device):
-            check(lib().pcops_gather_points(ptr(features), ptr(idx), B, C, N, M, ptr(out), stream_of(features)),
-                  "gather_points")
+            call("gather_points", lib().pcops_gather_points, ptr(features), ptr(idx), B, C, N, M, ptr(out),
+                 stream_of(features))
         ctx.save_for_backward(idx, features)
         return out
 
     @staticmethod
+    @custom_bwd(device_type="cuda")
     def backward(ctx, grad_out):
         idx, features = ctx.saved_tensors
         B, C, N = features.shape
@@ -63,8 +68,8 @@ class GatherOperation(Function):
         grad_out = grad_out.contiguous()
         gp = torch.empty(B, C, N, dtype=torch.float32, device=grad_out.device)
         with torch.cuda.device(grad_out.device):
-            check(lib().pcops_gather_points_grad(ptr(grad_out), ptr(idx), B, C, N, M, ptr(gp), stream_of(grad_out)),
-                  "gather_points_grad")
+            call("gather_points_grad", lib().pcops_gather_points_grad, ptr(grad_out), ptr(idx), B, C, N, M, ptr(gp),
+                 stream_of(grad_out))
         return gp, None
 
 
@@ -73,6 +78,7 @@ gather_operation = GatherOperation.apply
 
 class ThreeNN(Function):
     @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, unknown, known):
         require_float(unknown, "unknowns")
         require_float(known, "knows")
@@ -81,12 +87,13 @@ class ThreeNN(Function):
         dist2 = torch.empty(B, n, 3, dtype=torch.float32, device=unknown.device)
         idx = torch.empty(B, n, 3, dtype=torch.int32, device=unknown.device)
         with torch.cuda.device(unknown.device):
-            check(lib().pcops_three_nn(ptr(unknown), ptr(known), B, n, m, ptr(dist2), ptr(idx), stream_of(unknown)),
-                  "three_nn")
+            call("three_nn", lib().pcops_three_nn, ptr(unknown), ptr(known), B, n, m, ptr(dist2), ptr(idx),
+                 stream_of(unknown))
         ctx.mark_non_differentiable(dist2, idx)
         return torch.sqrt(dist2), idx
 
     @staticmethod
+    @custom_bwd(device_type="cuda")
     def backward(ctx, grad_dist, grad_idx):
         return ()
 
@@ -96,6 +103,7 @@ three_nn = ThreeNN.apply
 
 class ThreeInterpolate(Function):
     @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, features, idx, weight):
         require_float(features, "points")
         require_int(idx, "idx")
@@ -105,11 +113,12 @@ class ThreeInterpolate(Function):
         ctx.save_for_backward(idx, weight, features)
         out = torch.empty(B, c, n, dtype=torch.float32, device=features.device)
         with torch.cuda.device(features.device):
-            check(lib().pcops_three_interpolate(ptr(features), ptr(idx), ptr(weight), B, c, m, n, ptr(out),
-                                                stream_of(features)), "three_interpolate")
+            call("three_interpolate", lib().pcops_three_interpolate, ptr(features), ptr(idx), ptr(weight), B, c, m, n,
+                 ptr(out), stream_of(features))
         return out
 
     @staticmethod
+    @custom_bwd(device_type="cuda")
     def backward(ctx, grad_out):
         idx, weight, features = ctx.saved_tensors
         B, c, m = features.shape
@@ -117,8 +126,8 @@ class ThreeInterpolate(Function):
         grad_out = grad_out.contiguous()
         gf = torch.empty(B, c, m, dtype=torch.float32, device=grad_out.device)
         with torch.cuda.device(grad_out.device):
-            check(lib().pcops_three_interpolate_grad(ptr(grad_out), ptr(idx), ptr(weight), B, c, n, m, ptr(gf),
-                                                     stream_of(grad_out)), "three_interpolate_grad")
+            call("three_interpolate_grad", lib().pcops_three_interpolate_grad, ptr(grad_out), ptr(idx), ptr(weight), B,
+                 c, n, m, ptr(gf), stream_of(grad_out))
         return gf, torch.zeros_like(idx), torch.zeros_like(weight)
 
 
@@ -127,6 +136,7 @@ three_interpolate = ThreeInterpolate.apply
 
 class GroupingOperation(Function):
     @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, features, idx):
         require_float(features, "points")
         require_int(idx, "idx")
@@ -134,12 +144,13 @@ class GroupingOperation(Function):
         _, S, K = idx.shape
         out = torch.empty(B, C, S, K, dtype=torch.float32, device=features.device)
         with torch.cuda.device(features.device):
-            check(lib().pcops_group_points(ptr(features), ptr(idx), B, C, N, S, K, ptr(out), stream_of(features)),
-                  "group_points")
+            call("group_points", lib().pcops_group_points, ptr(features), ptr(idx), B, C, N, S, K, ptr(out),
+                 stream_of(features))
         ctx.save_for_backward(idx, features)
         return out
 
     @staticmethod
+    @custom_bwd(device_type="cuda")
     def backward(ctx, grad_out):
         idx, features = ctx.saved_tensors
         B, C, N = features.shape
@@ -147,8 +158,8 @@ class GroupingOperation(Function):
         grad_out = grad_out.contiguous()
         gf = torch.empty(B, C, N, dtype=torch.float32, device=grad_out.device)
         with torch.cuda.device(grad_out.device):
-            check(lib().pcops_group_points_grad(ptr(grad_out), ptr(idx), B, C, N, S, K, ptr(gf),
-                                                stream_of(grad_out)), "group_points_grad")
+            call("group_points_grad", lib().pcops_group_points_grad, ptr(grad_out), ptr(idx), B, C, N, S, K, ptr(gf),
+                 stream_of(grad_out))
         return gf, torch.zeros_like(idx)
 
 
@@ -157,6 +168,7 @@ grouping_operation = GroupingOperation.apply
 
 class BallQuery(Function):
     @staticmethod
+    @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, radius, nsample, xyz, new_xyz):
         require_float(new_xyz, "new_xyz")
         require_float(xyz, "xyz")
@@ -164,12 +176,13 @@ class BallQuery(Function):
         M = new_xyz.shape[1]
         out = torch.empty(B, M, int(nsample), dtype=torch.int32, device=xyz.device)
         with torch.cuda.device(xyz.device):
-            check(lib().pcops_ball_query(ptr(new_xyz), ptr(xyz), B, N, M, float(radius), int(nsample), ptr(out),
-                                         stream_of(xyz)), "ball_query")
+            call("ball_query", lib().pcops_ball_query, ptr(new_xyz), ptr(xyz), B, N, M, float(radius), int(nsample),
+                 ptr(out), stream_of(xyz))
         ctx.mark_non_differentiable(out)
         return out
 
     @staticmethod
+    @custom_bwd(device_type="cuda")
     def backward(ctx, grad_out):
         return ()
 

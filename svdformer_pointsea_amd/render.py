@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import check, lib, ptr, require_float, stream_of
+from ._lib import call, lib, ptr, require_float, stream_of
 
 
 def euler2mat(angle):
@@ -59,8 +59,8 @@ class PCViews:
         wsb = lib().pcops_points2depth_workspace_bytes(B, V, R, R)
         ws = _lib.Workspace.get(points.device, wsb)
         with torch.cuda.device(points.device):
-            check(lib().pcops_points2depth(ptr(points), ptr(rot), ptr(trans), B, N, V, R, R, ptr(img), ptr(ws), wsb,
-                                           stream_of(points)), "points2depth")
+            call("points2depth", lib().pcops_points2depth, ptr(points), ptr(rot), ptr(trans), B, N, V, R, R, ptr(img),
+                 ptr(ws), wsb, stream_of(points))
         return img
 
 
@@ -125,8 +125,8 @@ class PCViews_Real:
         rot, rot2, trans, _ = self._consts(points.device)
         grid = torch.empty(B * V, D, R, R, device=points.device)
         with torch.cuda.device(points.device):
-            check(lib().pcops_points2grid(ptr(points), ptr(rot), ptr(rot2), ptr(trans), B, N, V, R, D, ptr(grid),
-                                          stream_of(points)), "points2grid")
+            call("points2grid", lib().pcops_points2grid, ptr(points), ptr(rot), ptr(rot2), ptr(trans), B, N, V, R, D,
+                 ptr(grid), stream_of(points))
         return grid
 
     def grid2image(self, grid):
@@ -138,8 +138,8 @@ class PCViews_Real:
         wsb = lib().pcops_grid2image_workspace_bytes(BV, D, R)
         ws = _lib.Workspace.get(grid.device, wsb)
         with torch.cuda.device(grid.device):
-            check(lib().pcops_grid2image(ptr(grid), ptr(kern), BV, D, R, ptr(img), ptr(ws), wsb, stream_of(grid)),
-                  "grid2image")
+            call("grid2image", lib().pcops_grid2image, ptr(grid), ptr(kern), BV, D, R, ptr(img), ptr(ws), wsb,
+                 stream_of(grid))
         return img
 
     def get_img(self, points):

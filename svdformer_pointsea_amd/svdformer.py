@@ -1,0 +1,441 @@
+"""SVDFormer (models/SVDFormer.py, ICCV'23) restated as the caller of this
+package's hot path, so the PCN train step (core/train_pcn.py:101-134) runs
+end to end on MI355X with every point op and attention core on libpcops.so.
+
+Module / attribute names follow the reference (encoder, localencoder,
+refine1, refine2, ... down to conv / norm names) so a reference state_dict
+loads with strict=True.  Dense layers (ResNet image branch, 1x1 convs,
+LayerNorm, GELU, BatchNorm) are plain torch (MIOpen / hipBLASLt).
+
+Reference map:
+  Conv2d / MLP_CONV / PCSA / PointNet_SA_Module_KNN   models/model_utils.py:27-487
+  EdgeConv / SinusoidalPositionalEmbedding            models/model_utils.py:847-917
+  FeatureExtractor / SDG / SVFNet / local_encoder / Model   models/SVDFormer.py:11-204
+  ResNet BasicBlock layers (feature_size 16)           models/resnet.py:36-240
+  get_loss / chamfer_sqrt                             utils/loss_utils.py:10-58
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .attention import SDG_Decoder, cross_attention, self_attention
+from .chamfer3D import chamfer_3DDist
+from .model_utils import fps_subsample, group_local, sample_and_group_knn
+from .pointnet2_utils import furthest_point_sample, gather_operation
+
+
+# ----------------------------------------------------------------- blocks
+class Conv2d(nn.Module):
+    """model_utils.py:27-43."""
+
+    def __init__(self, in_channel, out_channel, kernel_size=(1, 1), stride=(1, 1), if_bn=True,
+                 activation_fn=torch.relu):
+        super().__init__()
+        self.conv = nn.Conv2d(in_channel, out_channel, kernel_size, stride=stride)
+        self.if_bn = if_bn
+        self.bn = nn.BatchNorm2d(out_channel)
+        self.activation_fn = activation_fn
+
+    def forward(self, x):
+        out = self.conv(x)
+        if self.if_bn:
+            out = self.bn(out)
+        if self.activation_fn is not None:
+            out = self.activation_fn(out)
+        return out
+
+
+class MLP_CONV(nn.Module):
+    """model_utils.py:62-78 (1x1 Conv1d stack, ReLU between, no BN by default)."""
+
+    def __init__(self, in_channel, layer_dims, bn=None):
+        super().__init__()
+        layers = []
+        last = in_channel
+        for out_channel in layer_dims[:-1]:
+            layers.append(nn.Conv1d(last, out_channel, 1))
+            if bn:
+                layers.append(nn.BatchNorm1d(out_channel))
+            layers.append(nn.ReLU())
+            last = out_channel
+        layers.append(nn.Conv1d(last, layer_dims[-1], 1))
+        self.mlp = nn.Sequential(*layers)
+
+    def forward(self, x):
+        return self.mlp(x)
+
+
+class PCSA(nn.Module):
+    """Point Cloud Spectral Adapter (model_utils.py:358-430): orthonormal DCT-II
+    along the neighbourhood axis, channel-averaged frequency gates, inverse DCT."""
+
+    def __init__(self, channels, k_neighbors):
+        super().__init__()
+        self.channels = channels
+        self.k = k_neighbors if k_neighbors is not None else 0
+        self.freq_mlp = None
+        if self.k > 0:
+            hidden = max(8, self.k // 2)
+            self.freq_mlp = nn.Sequential(nn.Linear(self.k, hidden), nn.GELU(), nn.Linear(hidden, self.k),
+                                          nn.Sigmoid())
+        self._bases = {}
+
+    def _dct(self, device, dtype):
+        key = (device, dtype)
+        if key not in self._bases:
+            n = self.k
+            x = torch.arange(n, device=device, dtype=dtype).view(1, -1)
+            u = torch.arange(n, device=device, dtype=dtype).view(-1, 1)
+            pi = torch.tensor(np.pi, device=device, dtype=dtype)
+            mat = torch.cos((pi / n) * (x + 0.5) * u)
+            mat *= (2.0 / n) ** 0.5
+            mat[0, :] *= 0.5 ** 0.5
+            self._bases[key] = (mat, mat.transpose(0, 1).contiguous())
+        return self._bases[key]
+
+    def forward(self, x):
+        if self.k == 0 or self.freq_mlp is None:
+            return x
+        B, C, S, K = x.shape
+        dct, idct = self._dct(x.device, x.dtype)
+        x_flat = x.permute(0, 2, 1, 3).contiguous().view(B * S * C, K)
+        spec = torch.matmul(x_flat, dct.t())
+        gates = self.freq_mlp(x.mean(dim=1)).view(B * S, K)
+        gates = gates.unsqueeze(1).repeat(1, C, 1).view(B * S * C, K)
+        spec = spec * gates
+        out = torch.matmul(spec, idct.t())
+        return out.view(B, S, C, K).permute(0, 2, 1, 3).contiguous()
+
+
+def sample_and_group_all(xyz, points, use_xyz=True):
+    """model_utils.py:129-156."""
+    b, _, nsample = xyz.shape
+    new_xyz = torch.zeros((1, 3, 1), dtype=torch.float, device=xyz.device).repeat(b, 1, 1)
+    grouped_xyz = xyz.reshape((b, 3, 1, nsample))
+    idx = torch.arange(nsample, device=xyz.device).reshape(1, 1, nsample).repeat(b, 1, 1)
+    if points is not None:
+        new_points = torch.cat([xyz, points], 1) if use_xyz else points
+        new_points = new_points.unsqueeze(2)
+    else:
+        new_points = grouped_xyz
+    return new_xyz, new_points, idx, grouped_xyz
+
+
+class PointNet_SA_Module_KNN(nn.Module):
+    """model_utils.py:432-487."""
+
+    def __init__(self, npoint, nsample, in_channel, mlp, if_bn=True, group_all=False, use_xyz=True, if_idx=False,
+                 use_pcsa=False):
+        super().__init__()
+        self.npoint, self.nsample, self.mlp = npoint, nsample, mlp
+        self.group_all, self.use_xyz, self.if_idx, self.use_pcsa = group_all, use_xyz, if_idx, use_pcsa
+        if use_xyz:
+            in_channel += 3
+        last = in_channel
+        convs = []
+        for out_channel in mlp[:-1]:
+            convs.append(Conv2d(last, out_channel, if_bn=if_bn))
+            last = out_channel
+        convs.append(Conv2d(last, mlp[-1], if_bn=False, activation_fn=None))
+        self.mlp_conv = nn.Sequential(*convs)
+        self.pcsa = PCSA(mlp[-1], nsample) if (not group_all and use_pcsa) else None
+
+    def forward(self, xyz, points, idx=None):
+        if self.group_all:
+            new_xyz, new_points, idx, _ = sample_and_group_all(xyz, points, self.use_xyz)
+        else:
+            new_xyz, new_points, idx, _ = sample_and_group_knn(xyz, points, self.npoint, self.nsample, self.use_xyz,
+                                                               idx=idx)
+        new_points = self.mlp_conv(new_points)
+        if self.pcsa is not None:
+            new_points = self.pcsa(new_points)
+        new_points = torch.max(new_points, 3)[0]
+        return (new_xyz, new_points, idx) if self.if_idx else (new_xyz, new_points)
+
+
+class EdgeConv(nn.Module):
+    """model_utils.py:847-881 (kNN in feature space -> edge features -> conv -> max)."""
+
+    def __init__(self, input_channel, output_channel, k):
+        super().__init__()
+        self.num_neigh = k
+        self.conv = nn.Sequential(
+            nn.Conv2d(2 * input_channel, output_channel // 2, kernel_size=1),
+            nn.BatchNorm2d(output_channel // 2),
+            nn.LeakyReLU(negative_slope=0.2),
+            nn.Conv2d(output_channel // 2, output_channel // 2, kernel_size=1),
+            nn.BatchNorm2d(output_channel // 2),
+            nn.LeakyReLU(negative_slope=0.2),
+            nn.Conv2d(output_channel // 2, output_channel, kernel_size=1))
+
+    def forward(self, inputs):
+        B, C, N = inputs.shape
+        if self.num_neigh is not None:
+            neigh = group_local(inputs.float(), k=self.num_neigh).contiguous().to(inputs.dtype)
+            central = inputs.unsqueeze(dim=3).repeat(1, 1, 1, self.num_neigh)
+        else:
+            central = torch.zeros(B, C, N, 1, device=inputs.device, dtype=inputs.dtype)
+            neigh = inputs.unsqueeze(-1)
+        feature = torch.cat((central - neigh, central), dim=1)
+        return self.conv(feature).max(dim=-1, keepdim=False)[0]
+
+
+class SinusoidalPositionalEmbedding(nn.Module):
+    """model_utils.py:883-917."""
+
+    def __init__(self, d_model):
+        super().__init__()
+        if d_model % 2 != 0:
+            raise ValueError(f"Sinusoidal positional encoding with odd d_model: {d_model}")
+        self.d_model = d_model
+        div_indices = torch.arange(0, d_model, 2).float()
+        self.register_buffer("div_term", torch.exp(div_indices * (-np.log(10000.0) / d_model)))
+
+    def forward(self, emb_indices):
+        shape = emb_indices.shape
+        omegas = emb_indices.reshape(-1, 1, 1) * self.div_term.view(1, -1, 1)
+        emb = torch.cat([torch.sin(omegas), torch.cos(omegas)], dim=2)
+        return emb.view(*shape, self.d_model).detach()
+
+
+class Squeeze(nn.Module):
+    def forward(self, inp):
+        return inp.squeeze()
+
+
+class BasicBlock(nn.Module):
+    """models/resnet.py:36-70 (torchvision BasicBlock)."""
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + identity)
+
+
+def _resnet_layers(feature_size=16, layers=(2, 2, 2, 2)):
+    """ResNet(BasicBlock, [2,2,2,2], feature_size=16, zero_init_residual=True) children 4..-1
+    (layer1-4 + avgpool), initialised as models/resnet.py:146-163."""
+    inplanes = feature_size
+    out = []
+    for i, n in enumerate(layers):
+        planes = feature_size * (2 ** i)
+        stride = 1 if i == 0 else 2
+        down = None
+        if stride != 1 or inplanes != planes:
+            down = nn.Sequential(nn.Conv2d(inplanes, planes, 1, stride=stride, bias=False), nn.BatchNorm2d(planes))
+        blocks = [BasicBlock(inplanes, planes, stride, down)]
+        inplanes = planes
+        blocks += [BasicBlock(inplanes, planes) for _ in range(1, n)]
+        out.append(nn.Sequential(*blocks))
+    out.append(nn.AdaptiveAvgPool2d((1, 1)))
+    for m in nn.Sequential(*out).modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        elif isinstance(m, nn.BatchNorm2d):
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+    for m in nn.Sequential(*out).modules():
+        if isinstance(m, BasicBlock):
+            nn.init.constant_(m.bn2.weight, 0)
+    return out, inplanes
+
+
+# ----------------------------------------------------------------- SVDFormer
+class FeatureExtractor(nn.Module):
+    """SVDFormer.py:11-36."""
+
+    def __init__(self, out_dim=256, use_pcsa=True):
+        super().__init__()
+        self.sa_module_1 = PointNet_SA_Module_KNN(512, 16, 3, [64, 128], group_all=False, if_bn=False, if_idx=True,
+                                                  use_pcsa=use_pcsa)
+        self.sa_module_2 = PointNet_SA_Module_KNN(128, 16, 128, [128, 256], group_all=False, if_bn=False,
+                                                  if_idx=True, use_pcsa=use_pcsa)
+        self.sa_module_3 = PointNet_SA_Module_KNN(None, None, 256, [512, out_dim], group_all=True, if_bn=False,
+                                                  use_pcsa=False)
+
+    def forward(self, point_cloud):
+        l1_xyz, l1_points, _ = self.sa_module_1(point_cloud, point_cloud)
+        l2_xyz, l2_points, _ = self.sa_module_2(l1_xyz, l1_points)
+        _, l3_points = self.sa_module_3(l2_xyz, l2_points)
+        return l3_points
+
+
+class SDG(nn.Module):
+    """SVDFormer.py:38-104: structure analysis + similarity alignment decoder."""
+
+    def __init__(self, channel=128, ratio=1, hidden_dim=512, dataset="ShapeNet"):
+        super().__init__()
+        self.channel, self.hidden, self.ratio = channel, hidden_dim, ratio
+        self.conv_1 = nn.Conv1d(256, channel, kernel_size=1)
+        self.conv_11 = nn.Conv1d(512, 256, kernel_size=1)
+        self.conv_x = nn.Conv1d(3, 64, kernel_size=1)
+        self.sa1 = self_attention(channel * 2, hidden_dim, dropout=0.0, nhead=8)
+        self.cross1 = cross_attention(hidden_dim, hidden_dim, dropout=0.0, nhead=8)
+        if dataset == "ShapeNet":
+            self.decoder1 = SDG_Decoder(hidden_dim, channel, ratio)
+            self.decoder2 = SDG_Decoder(hidden_dim, channel, ratio)
+        else:
+            self.decoder1 = self_attention(hidden_dim, channel * ratio, dropout=0.0, nhead=8)
+            self.decoder2 = self_attention(hidden_dim, channel * ratio, dropout=0.0, nhead=8)
+        self.relu = nn.GELU()
+        self.conv_out = nn.Conv1d(64, 3, kernel_size=1)
+        self.conv_delta = nn.Conv1d(channel, channel * 1, kernel_size=1)
+        self.conv_ps = nn.Conv1d(channel * ratio * 2, channel * ratio, kernel_size=1)
+        self.conv_x1 = nn.Conv1d(64, channel, kernel_size=1)
+        self.conv_out1 = nn.Conv1d(channel, 64, kernel_size=1)
+        self.mlpp = MLP_CONV(in_channel=256, layer_dims=[256, hidden_dim])
+        self.sigma = 0.2
+        self.embedding = SinusoidalPositionalEmbedding(hidden_dim)
+        self.cd_distance = chamfer_3DDist()
+
+    def forward(self, local_feat, coarse, f_g, partial):
+        batch_size, _, N = coarse.size()
+        F_ = self.conv_x1(self.relu(self.conv_x(coarse)))
+        f_g = self.conv_1(self.relu(self.conv_11(f_g)))
+        F_ = torch.cat([F_, f_g.repeat(1, 1, F_.shape[-1])], dim=1)
+        # structure analysis: half Chamfer distance to the partial input
+        half_cd = self.cd_distance(coarse.transpose(1, 2).float().contiguous(),
+                                   partial.transpose(1, 2).float().contiguous())[0] / self.sigma
+        # raw reshape of (B, N, hidden) to (B, hidden, N) (reference quirk, SVDFormer.py:77)
+        embd = self.embedding(half_cd).reshape(batch_size, self.hidden, -1).permute(2, 0, 1)
+        F_Q = self.sa1(F_, embd)
+        F_Q_ = self.decoder1(F_Q)
+        # similarity alignment with the local features
+        local_feat = self.mlpp(local_feat)
+        F_H = self.cross1(F_Q, local_feat)
+        F_H_ = self.decoder2(F_H)
+        F_L = self.conv_delta(self.conv_ps(torch.cat([F_Q_, F_H_], 1)).reshape(batch_size, -1, N * self.ratio))
+        O_L = self.conv_out(self.relu(self.conv_out1(F_L)))
+        return coarse.repeat(1, 1, self.ratio) + O_L
+
+
+class SVFNet(nn.Module):
+    """SVDFormer.py:106-173: shape-view fusion encoder (image + point branches)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.channel = 64
+        self.point_feature_extractor = FeatureExtractor(use_pcsa=getattr(cfg.NETWORK, "USE_PCSA", True))
+        self.view_distance = cfg.NETWORK.view_distance
+        self.relu = nn.GELU()
+        self.sa = self_attention(self.channel * 8, self.channel * 8, dropout=0.0)
+        self.viewattn = self_attention(128 + 256, 256)
+        self.conv_out = nn.Conv1d(64, 3, kernel_size=1)
+        self.conv_out1 = nn.Conv1d(512 + self.channel * 4, 64, kernel_size=1)
+        self.ps = nn.ConvTranspose1d(512, self.channel, 128, bias=True)
+        self.ps_refuse = nn.Conv1d(512 + self.channel, self.channel * 8, kernel_size=1)
+        res_layers, _ = _resnet_layers(feature_size=16)
+        self.img_feature_extractor = nn.Sequential(
+            nn.Conv2d(1, 16, kernel_size=(3, 3), stride=(1, 1), padding=(1, 1), bias=False),
+            nn.BatchNorm2d(16, eps=1e-05, momentum=0.1, affine=True, track_running_stats=True),
+            nn.ReLU(inplace=True), *res_layers, Squeeze())
+        self.posmlp = MLP_CONV(3, [64, 256])
+
+    def forward(self, points, depth):
+        batch_size, _, N = points.size()
+        f_v = self.img_feature_extractor(depth).view(batch_size, 3, -1).transpose(1, 2).contiguous()
+        f_p = self.point_feature_extractor(points)
+        d = self.view_distance
+        view_point = torch.tensor([0, 0, -d, -d, 0, 0, 0, d, 0], dtype=torch.float32, device=depth.device)
+        view_point = view_point.view(-1, 3, 3).permute(0, 2, 1).expand(batch_size, 3, 3)
+        view_feature = self.posmlp(view_point).permute(2, 0, 1)
+        f_v_ = self.viewattn(torch.cat([f_v, f_p.repeat(1, 1, f_v.size(2))], 1), view_feature)
+        f_v_ = F.adaptive_max_pool1d(f_v_, 1)
+        f_g = torch.cat([f_p, f_v_], 1)
+        x = self.relu(self.ps(f_g))
+        x = self.relu(self.ps_refuse(torch.cat([x, f_g.repeat(1, 1, x.size(2))], 1)))
+        x2_d = (self.sa(x)).reshape(batch_size, self.channel * 4, N // 8)
+        coarse = self.conv_out(self.relu(self.conv_out1(torch.cat([x2_d, f_g.repeat(1, 1, x2_d.size(2))], 1))))
+        return f_g, coarse
+
+
+class local_encoder(nn.Module):
+    """SVDFormer.py:175-189."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.gcn_1 = EdgeConv(3, 64, 16)
+        self.gcn_2 = EdgeConv(64, 256, 8)
+        self.local_number = cfg.NETWORK.local_points
+
+    def forward(self, inp):
+        x1 = self.gcn_1(inp)
+        idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
+        x1 = gather_operation(x1.float().contiguous(), idx)
+        return self.gcn_2(x1)
+
+
+class Model(nn.Module):
+    """SVDFormer.py:191-204: (partial (B,N,3), depth (3B,1,224,224)) -> (coarse, fine1, fine2)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.encoder = SVFNet(cfg)
+        self.localencoder = local_encoder(cfg)
+        self.merge_points = cfg.NETWORK.merge_points
+        dataset = getattr(getattr(cfg, "DATASET", None), "TEST_DATASET", "ShapeNet")
+        self.refine1 = SDG(ratio=cfg.NETWORK.step1, hidden_dim=768, dataset=dataset)
+        self.refine2 = SDG(ratio=cfg.NETWORK.step2, hidden_dim=512, dataset=dataset)
+
+    def forward(self, partial, depth):
+        partial = partial.transpose(1, 2).contiguous()
+        feat_g, coarse = self.encoder(partial, depth)
+        local_feat = self.localencoder(partial)
+        coarse_merge = torch.cat([partial, coarse.to(partial.dtype)], dim=2).float().contiguous()
+        coarse_merge = gather_operation(coarse_merge, furthest_point_sample(coarse_merge.transpose(1, 2).contiguous(),
+                                                                            self.merge_points))
+        fine1 = self.refine1(local_feat, coarse_merge, feat_g, partial)
+        fine2 = self.refine2(local_feat, fine1, feat_g, partial)
+        return (coarse.transpose(1, 2).contiguous(), fine1.transpose(1, 2).contiguous(),
+                fine2.transpose(1, 2).contiguous())
+
+
+# ----------------------------------------------------------------- loss
+_chamfer = chamfer_3DDist()
+
+
+def chamfer_sqrt(p1, p2):
+    """utils/loss_utils.py:15-19: (mean sqrt d1 + mean sqrt d2) / 2."""
+    d1, d2, _, _ = _chamfer(p1.float(), p2.float())
+    return (torch.mean(torch.sqrt(d1)) + torch.mean(torch.sqrt(d2))) / 2
+
+
+def get_loss(pcds_pred, gt, sqrt=True, alpha1=1, alpha2=1):
+    """utils/loss_utils.py:33-58 (sqrt=True path used by train_pcn.py:111)."""
+    if not sqrt:
+        raise NotImplementedError("train_pcn uses sqrt=True")
+    Pc, P1, P2 = pcds_pred
+    gt_1 = fps_subsample(gt, P1.shape[1])
+    gt_c = fps_subsample(gt_1, Pc.shape[1])
+    cdc = chamfer_sqrt(Pc, gt_c)
+    cd1 = chamfer_sqrt(P1, gt_1)
+    cd2 = chamfer_sqrt(P2, gt)
+    return cdc + alpha1 * cd1 + alpha2 * cd2, [cdc, cd1, cd2]
+
+
+class PCNConfig:
+    """The NETWORK keys of config_pcn.py:54-60 the model reads."""
+
+    class NETWORK:
+        N_SAMPLING_POINTS = 2048
+        step1 = 4
+        step2 = 8
+        merge_points = 512
+        local_points = 512
+        view_distance = 0.7
+        USE_PCSA = True
+
+    class DATASET:
+        TEST_DATASET = "ShapeNet"
