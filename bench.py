@@ -1,0 +1,294 @@
+"""Headline benchmark: SVDFormer PCN train-step samples/s on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+One step = one iteration of core/train_pcn.py:101-134 on a synthetic
+PCN-shaped batch resident in HBM: depth render of the partial cloud
+(PCViews) -> SVDFormer forward (models/SVDFormer.py) -> get_loss (three
+sqrt-Chamfers, utils/loss_utils.py:33-58) -> backward -> Adam step.  The
+model is randomly initialised (no checkpoints offline), 58.09 M parameters,
+B=32 samples per GPU (configs[2] of BASELINE.json: bf16 autocast; point ops
+stay fp32 inside).  Every point op and every attention core runs on
+libpcops.so (hand-written gfx950 HIP); dense layers are torch (MIOpen /
+hipBLASLt).  N>1: one process per GPU, batch-partitioned (weak scaling),
+gradients all-reduced over RCCL by DDP -- the only data-path collective.
+
+Rank 0 prints ONE JSON line (the driver's contract) with, in addition:
+  roofline      -- dominant kernel: algorithmic FLOP (or bytes) per launch
+                   / mean launch duration, HIP events on the launch stream
+                   over the timed steps (DESIGN.md "Measurement");
+  cpu_baseline  -- the same train step on the host CPU for a bounded sample
+                   (oracle/cpu_path.py: torch CPU + the C restatement of the
+                   point ops), rank 0 at N=1 only;
+  kernels       -- every libpcops call's launches / mean ms / roofline frac;
+  composite_fps_knn_chamfer -- sum of roofline times / sum of measured
+                   times for the FPS + kNN + Chamfer launches.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12          # B/s, MI355X_MICROARCH.md (spec)
+MFMA_BF16_PEAK = 2.5e15    # FLOP/s dense
+MFMA_F32_PEAK = 157.3e12   # FLOP/s (f32 MFMA == f32 vector peak)
+VALU_F32_PEAK = 157.3e12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="samples per GPU")
+    ap.add_argument("--fp32", action="store_true", help="no bf16 autocast (configs[1] numerics)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------ data
+def synth_pcn(B, seed, device):
+    """PCN-shaped synthetic batch: gt (B,16384,3) on random rotated
+    ellipsoid surfaces inside the unit cube; partial (B,2048,3) = the half
+    facing a random view, resampled to 2048 with replacement (the PCN
+    loader's RandomSamplePoints)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    d = torch.randn(B, 16384, 3, generator=g)
+    d = d / d.norm(dim=-1, keepdim=True)
+    axes = 0.15 + 0.3 * torch.rand(B, 1, 3, generator=g)
+    q, _ = torch.linalg.qr(torch.randn(B, 3, 3, generator=g))
+    gt = torch.bmm(d * axes, q)
+    view = torch.randn(B, 3, generator=g)
+    partial = torch.empty(B, 2048, 3)
+    for b in range(B):
+        vis = gt[b][(d[b] @ (view[b] / view[b].norm())) > 0]
+        pick = torch.randint(0, vis.shape[0], (2048,), generator=g)
+        partial[b] = vis[pick]
+    return partial.contiguous().to(device), gt.contiguous().to(device)
+
+
+# ------------------------------------------------------------------ roofline model
+def kernel_work(name, a):
+    """(algorithmic amount, unit, peak, bound) for one libpcops call with int args `a`.
+
+    Per-unit figures are SURVEY.md 8(d)'s, restated in DESIGN.md:
+      attention fwd   4*BH*Lq*Lk*D FLOP (QK^T + PV)
+      attention dkv   8*BH*Lq*Lk*D FLOP (S recompute, dP, dV, dK)
+      attention dq    2*BH*Lq*Lk*D FLOP (dQ only; the S/dP recompute in this
+                      pass is overhead, not credited -- FA2's 10*BH*Lq*Lk*D
+                      total backward count)
+      FPS             16 B per point-iteration, B*N*M of them (HBM model)
+      Chamfer fwd     8 FLOP per pair, 2*B*N*M pairs (both directions)
+      kNN             (2C+2) FLOP per (query, candidate) pair (distance part)
+    """
+    if name == "attention forward":
+        BH, Lq, Lk, D, dt = a[5], a[6], a[7], a[8], a[10]
+        return 4.0 * BH * Lq * Lk * D, "TFLOP/s", MFMA_BF16_PEAK if dt == 1 else MFMA_F32_PEAK, "mfma"
+    if name == "attention bwd dkv":
+        BH, Lq, Lk, D, dt = a[7], a[8], a[9], a[10], a[12]
+        return 8.0 * BH * Lq * Lk * D, "TFLOP/s", MFMA_BF16_PEAK if dt == 1 else MFMA_F32_PEAK, "mfma"
+    if name == "attention bwd dq":
+        BH, Lq, Lk, D, dt = a[6], a[7], a[8], a[9], a[11]
+        return 2.0 * BH * Lq * Lk * D, "TFLOP/s", MFMA_BF16_PEAK if dt == 1 else MFMA_F32_PEAK, "mfma"
+    if name == "attention bwd delta":
+        BH, Lq, D, dt = a[2], a[3], a[4], a[5]
+        return (2.0 * BH * Lq * D * (4 if dt == 0 else 2) + 4.0 * BH * Lq), "GB/s", HBM_PEAK, "hbm"
+    if name == "furthest_point_sampling":
+        B, N, M = a[1], a[2], a[3]
+        return 16.0 * B * N * M, "GB/s", HBM_PEAK, "hbm"
+    if name == "chamfer_3D.forward":
+        B, N, M = a[2], a[3], a[4]
+        return 8.0 * 2 * B * N * M, "TFLOP/s", VALU_F32_PEAK, "valu"
+    if name == "knn":
+        B, S, N, C = a[2], a[3], a[4], a[5]
+        return (2.0 * C + 2) * B * S * N, "TFLOP/s", VALU_F32_PEAK, "valu"
+    return None
+
+
+def kernel_table(spans):
+    """Group recorded calls by (name, shape) and attach roofline fractions."""
+    rows = {}
+    for name, evs in spans.items():
+        for e0, e1, args in evs:
+            key = name
+            if name.startswith("attention") and name != "attention bwd delta":
+                d = {"attention forward": 8, "attention bwd dq": 9, "attention bwd dkv": 10}[name]
+                key = f"{name} [D={args[d]}, {'bf16' if args[d + 2] == 1 else 'fp32'}]"
+            r = rows.setdefault(key, {"name": name, "launches": 0, "ms": 0.0, "work": 0.0})
+            r["launches"] += 1
+            r["ms"] += e0.elapsed_time(e1)
+            w = kernel_work(name, args)
+            if w is not None:
+                r["work"] += w[0]
+                r["unit"], r["peak"], r["bound"] = w[1], w[2], w[3]
+    for r in rows.values():
+        if "peak" in r and r["ms"] > 0:
+            rate = r["work"] / (r["ms"] * 1e-3)
+            r["achieved"] = rate / (1e12 if r["unit"] == "TFLOP/s" else 1e9)
+            r["frac"] = rate / r["peak"]
+            r["roof_ms"] = r["work"] / r["peak"] * 1e3
+    return rows
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline(steps):
+    """The same train step on host cores for a bounded sample (1 sample/step)."""
+    from oracle.cpu_path import cpu_ops, depth_images
+    from svdformer_pointsea_amd.render import PCViews
+    from svdformer_pointsea_amd.svdformer import Model, PCNConfig, get_loss
+
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(nthreads)
+    torch.manual_seed(0)
+    model = Model(PCNConfig)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
+    render = PCViews(TRANS=-PCNConfig.NETWORK.view_distance, RESOLUTION=224)
+    partial, gt = synth_pcn(1, 12345, "cpu")
+
+    def step():
+        depth = depth_images(render, partial).unsqueeze(1)
+        loss, _ = get_loss(model(partial, depth), gt)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+
+    with cpu_ops():
+        step()  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "samples/s", "cores": nthreads, "kind": "port",
+            "sample": f"{steps} train steps of 1 PCN sample (2048->16384) after 1 warm-up, fp32: torch CPU "
+                      f"({nthreads} threads) + oracle/pcops_oracle.c point ops (1 thread) + torch CPU attention"}
+
+
+# ------------------------------------------------------------------ main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    import svdformer_pointsea_amd as pkg
+    from svdformer_pointsea_amd import _lib
+    from svdformer_pointsea_amd.render import PCViews
+    from svdformer_pointsea_amd.svdformer import Model, PCNConfig, get_loss
+
+    pkg.lib()  # fail loudly if libpcops.so is missing
+    torch.manual_seed(0)  # identical init on every rank
+    model = Model(PCNConfig).to(device)
+    nparams = sum(p.numel() for p in model.parameters())
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[local], broadcast_buffers=False, gradient_as_bucket_view=True, bucket_cap_mb=64,
+            static_graph=True)  # the if_bn=False Conv2d blocks own BatchNorms that get no grad
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999), weight_decay=0, fused=True)
+    render = PCViews(TRANS=-PCNConfig.NETWORK.view_distance, RESOLUTION=224)
+    partial, gt = synth_pcn(args.batch, 1000 + rank, device)
+    loss_acc = torch.zeros((), device=device)
+    amp = not args.fp32
+
+    def step():
+        nonlocal loss_acc
+        depth = render.get_img(partial).unsqueeze(1)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            pcds = model(partial, depth)
+            loss, _ = get_loss(pcds, gt)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        loss_acc = loss_acc + loss.detach()  # logged without a host sync
+
+    for _ in range(args.warmup):
+        step()
+    if not args.no_kernel_timing:
+        _lib.KernelTimer.enable()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    spans = _lib.KernelTimer.spans or {}
+    _lib.KernelTimer.disable()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if not math.isfinite(loss_acc.item()):
+        raise RuntimeError("non-finite loss in the timed steps")
+
+    rows = kernel_table(spans)
+    out = None
+    if rank == 0:
+        samples = args.batch * world * args.steps
+        out = {
+            "metric": "train-step samples/sec (PCN, B=32, 2048->16384 pts)",
+            "value": samples / elapsed,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.fp32 else "bf16",
+            "data": "synthetic (random ellipsoid-surface PCN-shaped clouds, random-init weights)",
+            "config": {"workload": "SVDFormer PCN train step: render + fwd + get_loss + bwd + Adam",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch, "points_in": 2048,
+                       "points_out": 16384, "params": nparams,
+                       "parallelism": f"dp{world}" if world > 1 else "single"},
+        }
+        timed = {k: r for k, r in rows.items() if "frac" in r}
+        if timed:
+            dom_key = max(timed, key=lambda k: timed[k]["ms"])
+            d = timed[dom_key]
+            out["roofline"] = {"kernel": dom_key, "bound": d["bound"], "achieved": round(d["achieved"], 2),
+                               "peak": d["peak"] / (1e12 if d["unit"] == "TFLOP/s" else 1e9), "unit": d["unit"],
+                               "frac": round(d["frac"], 4), "traffic": None,
+                               "avg_launch_ms": round(d["ms"] / d["launches"], 4),
+                               "work_per_launch": d["work"] / d["launches"]}
+            group = [r for r in timed.values() if r["name"] in ("furthest_point_sampling", "knn",
+                                                                 "chamfer_3D.forward")]
+            if group:
+                out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) /
+                                                         sum(r["ms"] for r in group), 4)
+            step_ms = elapsed * 1e3 / args.steps
+            out["kernels"] = {k: {"launches_per_step": r["launches"] / args.steps,
+                                  "ms_per_step": round(r["ms"] / args.steps, 4),
+                                  "share": round(r["ms"] / args.steps / step_ms, 4),
+                                  **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {})}
+                              for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_steps)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

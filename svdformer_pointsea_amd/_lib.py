@@ -99,7 +99,7 @@ class KernelTimer:
     current stream of the current device), so spans are exact per call even
     when the caller uses side streams.  Used by bench.py; off by default."""
 
-    spans = None  # name -> [(start_event, end_event)] while enabled
+    spans = None  # name -> [(start_event, end_event, scalar args)] while enabled
 
     @classmethod
     def enable(cls):
@@ -119,7 +119,7 @@ class KernelTimer:
         """name -> (launches, mean ms, total ms); call after synchronising."""
         out = {}
         for name, evs in (cls.spans or {}).items():
-            ms = [a.elapsed_time(b) for a, b in evs]
+            ms = [a.elapsed_time(b) for a, b, _ in evs]
             out[name] = (len(ms), sum(ms) / len(ms), sum(ms))
         return out
 
@@ -134,7 +134,8 @@ def call(what, fn, *args):
     e0.record(s)
     status = fn(*args)
     e1.record(s)
-    spans.setdefault(what, []).append((e0, e1))
+    scalars = tuple(a if isinstance(a, (int, float)) else None for a in args)
+    spans.setdefault(what, []).append((e0, e1, scalars))
     check(status, what)
 
 
