@@ -16,6 +16,8 @@
 // Precision: bf16 operands (v_mfma_f32_32x32x16_bf16, fp32 accumulate) for
 // speed, or fp32 operands (v_mfma_f32_32x32x2_f32, exact fp32 fma chain) for
 // the parity build.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -357,6 +359,462 @@ __global__ __launch_bounds__(kThreads) void attn_dkv_kernel(const T *__restrict_
   store_Y<T, D>(Y2, dK + bh * st.k_sbh, st.k_srow, k0w, Lk, scale);
 }
 
+// ----------------------------------------------------------------- forward, bf16 (v2)
+// NW waves x 32 queries per block; 64-key K/V tiles double-buffered in LDS
+// (dynamic), the next tile prefetched into registers while the current one
+// is on the matrix cores; one barrier per tile.  Half-wave exchange by
+// v_permlane32_swap; the softmax scale folded into the exp2 argument (fma).
+constexpr int kKT = 64;  // keys per tile
+
+__device__ __forceinline__ float swap_halves_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float swap_halves_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// acc += Rows(32 x D, LDS row stride RS) . Ent   (entity fragment f)
+template <int D, int RS>
+__device__ __forceinline__ void k_product(f32x16 &acc, const __bf16 *lds, const bf16x8 (&f)[D / 16]) {
+  const int l = lane_(), h = l >> 5;
+  const __bf16 *rp = lds + (l & 31) * RS + 8 * h;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8 *>(rp + 16 * s);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, f[s], acc, 0, 0, 0);
+  }
+}
+
+// Y[db] += Rows^T(D x 32, LDS row stride RS) . X   (X = fp32 accumulator of 32 rows)
+template <int D, int RS>
+__device__ __forceinline__ void v_product(f32x16 (&Y)[D / 32], const __bf16 *lds, const f32x16 &X) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (__bf16)X[8 * s + e];
+    const int row0 = 16 * s + 4 * h + q;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      const int col = db * 32 + 16 * g + 4 * p;
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + row0 * RS + col));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + (row0 + 8) * RS + col));
+      const bf16x8 a = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1,
+                                               2, 3, 4, 5, 6, 7);
+      Y[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, Y[db], 0, 0, 0);
+    }
+  }
+#endif
+}
+
+template <int D, int NW>
+struct Fwd2Cfg {
+  static constexpr int kThr = NW * 64;
+  static constexpr int kKS = D + 8;                 // K tile row stride (b128 row reads)
+  static constexpr int kVS = D + 8;                 // V tile row stride (tr reads)
+  static constexpr int kChunks = kKT * D / 8;       // 16-B chunks per tile
+  static constexpr int kCPT = (kChunks + kThr - 1) / kThr;
+  static constexpr int kKBuf = kKT * kKS, kVBuf = kKT * kVS;
+  static constexpr size_t kLds = 2ull * (kKBuf + kVBuf) * sizeof(__bf16);
+  typedef bf16x8 Regs[kCPT];
+};
+
+template <int D, int NW>
+__device__ __forceinline__ void fwd2_load(typename Fwd2Cfg<D, NW>::Regs &kr, typename Fwd2Cfg<D, NW>::Regs &vr,
+                                          const __bf16 *Kb, long long ks, const __bf16 *Vb, long long vs, int k0,
+                                          int Lk) {
+  using C = Fwd2Cfg<D, NW>;
+#pragma unroll
+  for (int t = 0; t < C::kCPT; ++t) {
+    const int c = threadIdx.x + t * C::kThr;
+    const int row = c / (D / 8), ch = c % (D / 8);
+    const bool ok = (C::kChunks % C::kThr == 0 || c < C::kChunks) && k0 + row < Lk;
+    kr[t] = ok ? *reinterpret_cast<const bf16x8 *>(Kb + (long long)(k0 + row) * ks + ch * 8) : bf16x8{};
+    vr[t] = ok ? *reinterpret_cast<const bf16x8 *>(Vb + (long long)(k0 + row) * vs + ch * 8) : bf16x8{};
+  }
+}
+
+template <int D, int NW>
+__device__ __forceinline__ void fwd2_store(__bf16 *sk, __bf16 *sv, const typename Fwd2Cfg<D, NW>::Regs &kr,
+                                           const typename Fwd2Cfg<D, NW>::Regs &vr) {
+  using C = Fwd2Cfg<D, NW>;
+#pragma unroll
+  for (int t = 0; t < C::kCPT; ++t) {
+    const int c = threadIdx.x + t * C::kThr;
+    if (C::kChunks % C::kThr != 0 && c >= C::kChunks) continue;
+    const int row = c / (D / 8), ch = c % (D / 8);
+    *reinterpret_cast<bf16x8 *>(sk + row * C::kKS + ch * 8) = kr[t];
+    *reinterpret_cast<bf16x8 *>(sv + row * C::kVS + ch * 8) = vr[t];
+  }
+}
+
+template <int D, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
+                                                            const __bf16 *__restrict__ V, __bf16 *__restrict__ O,
+                                                            float *__restrict__ lse, int Lq, int Lk, float scale,
+                                                            Strides st) {
+  using C = Fwd2Cfg<D, NW>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char fwd2_smem[];
+  __bf16 *sk = reinterpret_cast<__bf16 *>(fwd2_smem);
+  __bf16 *sv = sk + 2 * C::kKBuf;
+  const int bh = blockIdx.y;
+  const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
+  const int q0 = blockIdx.x * (NW * 32) + w * 32;
+  const int qi = q0 + (l & 31);
+  bf16x8 qf[D / 16];
+  {
+    const __bf16 *row = Q + bh * st.q_sbh + (long long)(qi < Lq ? qi : 0) * st.q_srow + 8 * h;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) qf[s] = qi < Lq ? *reinterpret_cast<const bf16x8 *>(row + 16 * s) : bf16x8{};
+  }
+  const __bf16 *Kb = K + bh * st.k_sbh;
+  const __bf16 *Vb = V + bh * st.v_sbh;
+  const float sl2 = scale * kLog2e;
+  float m = -INFINITY, lsum = 0.f;
+  f32x16 Y[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) Y[db] = f32x16{};
+  typename C::Regs kr, vr;
+  fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
+  fwd2_store<D, NW>(sk, sv, kr, vr);
+  lds_barrier();
+  const int ntiles = (Lk + kKT - 1) / kKT;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const int k0 = t * kKT;
+    if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
+    const __bf16 *ck = sk + cur * C::kKBuf;
+    const __bf16 *cv = sv + cur * C::kVBuf;
+    f32x16 X0 = f32x16{}, X1 = f32x16{};
+    k_product<D, C::kKS>(X0, ck, qf);
+    k_product<D, C::kKS>(X1, ck + 32 * C::kKS, qf);
+    if (k0 + kKT > Lk) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (k0 + acc_row(r, h) >= Lk) X0[r] = -INFINITY;
+        if (k0 + 32 + acc_row(r, h) >= Lk) X1[r] = -INFINITY;
+      }
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(X0[r], X1[r]));
+    tmax = swap_halves_max(tmax);
+    const float mn = fmaxf(m, tmax * sl2);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      X0[r] = exp2f(__builtin_fmaf(X0[r], sl2, -mn));
+      X1[r] = exp2f(__builtin_fmaf(X1[r], sl2, -mn));
+      rs += X0[r] + X1[r];
+    }
+    rs = swap_halves_sum(rs);
+    lsum = lsum * alpha + rs;
+    m = mn;
+    if (alpha != 1.f) {
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) Y[db] *= alpha;
+    }
+    v_product<D, C::kVS>(Y, cv, X0);
+    v_product<D, C::kVS>(Y, cv + 32 * C::kVS, X1);
+    if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
+    lds_barrier();
+  }
+  store_Y<__bf16, D>(Y, O + bh * st.o_sbh, st.o_srow, q0, Lq, 1.f / lsum);
+  if (h == 0 && qi < Lq && lse) lse[(long long)bh * Lq + qi] = (m + log2f(lsum)) * kLn2;
+}
+
+template <int D, int NW>
+int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, float scale,
+                const Strides &st, hipStream_t s) {
+  using C = Fwd2Cfg<D, NW>;
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_fwd2_kernel<D, NW>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
+  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
+  const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
+  hipLaunchKernelGGL((attn_fwd2_kernel<D, NW>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (__bf16 *)o, lse, Lq, Lk, scale, st);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+// ----------------------------------------------------------------- backward, bf16 (v2)
+// dQ pass: queries on the lane, K/V 64-row tiles double-buffered (as forward).
+template <int D, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
+                                                           const __bf16 *__restrict__ V, const __bf16 *__restrict__ dO,
+                                                           const float *__restrict__ lse,
+                                                           const float *__restrict__ delta, __bf16 *__restrict__ dQ,
+                                                           int Lq, int Lk, float scale, Strides st) {
+  using C = Fwd2Cfg<D, NW>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char bwd2_smem[];
+  __bf16 *sk = reinterpret_cast<__bf16 *>(bwd2_smem);
+  __bf16 *sv = sk + 2 * C::kKBuf;
+  const int bh = blockIdx.y;
+  const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
+  const int q0 = blockIdx.x * (NW * 32) + w * 32;
+  const int qi = q0 + (l & 31);
+  const bool qv = qi < Lq;
+  bf16x8 qf[D / 16], gf[D / 16];
+  {
+    const __bf16 *qr = Q + bh * st.q_sbh + (long long)(qv ? qi : 0) * st.q_srow + 8 * h;
+    const __bf16 *gr = dO + bh * st.o_sbh + (long long)(qv ? qi : 0) * st.o_srow + 8 * h;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      qf[s] = qv ? *reinterpret_cast<const bf16x8 *>(qr + 16 * s) : bf16x8{};
+      gf[s] = qv ? *reinterpret_cast<const bf16x8 *>(gr + 16 * s) : bf16x8{};
+    }
+  }
+  const float lse2 = qv ? lse[(long long)bh * Lq + qi] * kLog2e : INFINITY;
+  const float dl = qv ? delta[(long long)bh * Lq + qi] : 0.f;
+  const __bf16 *Kb = K + bh * st.k_sbh;
+  const __bf16 *Vb = V + bh * st.v_sbh;
+  const float sl2 = scale * kLog2e;
+  f32x16 Y[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) Y[db] = f32x16{};
+  typename C::Regs kr, vr;
+  fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
+  fwd2_store<D, NW>(sk, sv, kr, vr);
+  lds_barrier();
+  const int ntiles = (Lk + kKT - 1) / kKT;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const int k0 = t * kKT;
+    if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
+    const __bf16 *ck = sk + cur * C::kKBuf;
+    const __bf16 *cv = sv + cur * C::kVBuf;
+    f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
+    k_product<D, C::kKS>(S0, ck, qf);
+    k_product<D, C::kKS>(S1, ck + 32 * C::kKS, qf);
+    k_product<D, C::kVS>(G0, cv, gf);
+    k_product<D, C::kVS>(G1, cv + 32 * C::kVS, gf);
+    const bool edge = k0 + kKT > Lk;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p0 = exp2f(__builtin_fmaf(S0[r], sl2, -lse2));
+      float p1 = exp2f(__builtin_fmaf(S1[r], sl2, -lse2));
+      if (edge) {
+        if (k0 + acc_row(r, h) >= Lk) p0 = 0.f;
+        if (k0 + 32 + acc_row(r, h) >= Lk) p1 = 0.f;
+      }
+      S0[r] = p0 * (G0[r] - dl);  // dS^T without the softmax scale
+      S1[r] = p1 * (G1[r] - dl);
+    }
+    v_product<D, C::kKS>(Y, ck, S0);
+    v_product<D, C::kKS>(Y, ck + 32 * C::kKS, S1);
+    if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
+    lds_barrier();
+  }
+  store_Y<__bf16, D>(Y, dQ + bh * st.q_sbh, st.q_srow, q0, Lq, scale);
+}
+
+// dK/dV pass: keys on the lane, Q/dO 64-row tiles (+ their lse/delta) double-buffered.
+template <int D, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_dkv2_kernel(const __bf16 *__restrict__ Q,
+                                                            const __bf16 *__restrict__ K,
+                                                            const __bf16 *__restrict__ V,
+                                                            const __bf16 *__restrict__ dO,
+                                                            const float *__restrict__ lse,
+                                                            const float *__restrict__ delta, __bf16 *__restrict__ dK,
+                                                            __bf16 *__restrict__ dV, int Lq, int Lk, float scale,
+                                                            Strides st) {
+  using C = Fwd2Cfg<D, NW>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char bwd2_smem[];
+  __bf16 *sq = reinterpret_cast<__bf16 *>(bwd2_smem);
+  __bf16 *sg = sq + 2 * C::kKBuf;
+  float *slse = reinterpret_cast<float *>(sg + 2 * C::kVBuf);  // [2][64]
+  float *sdl = slse + 2 * kKT;                                  // [2][64]
+  const int bh = blockIdx.y;
+  const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
+  const int k0w = blockIdx.x * (NW * 32) + w * 32;
+  const int ki = k0w + (l & 31);
+  const bool kv = ki < Lk;
+  bf16x8 kf[D / 16], vf[D / 16];
+  {
+    const __bf16 *kr0 = K + bh * st.k_sbh + (long long)(kv ? ki : 0) * st.k_srow + 8 * h;
+    const __bf16 *vr0 = V + bh * st.v_sbh + (long long)(kv ? ki : 0) * st.v_srow + 8 * h;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      kf[s] = kv ? *reinterpret_cast<const bf16x8 *>(kr0 + 16 * s) : bf16x8{};
+      vf[s] = kv ? *reinterpret_cast<const bf16x8 *>(vr0 + 16 * s) : bf16x8{};
+    }
+  }
+  const __bf16 *Qb = Q + bh * st.q_sbh;
+  const __bf16 *Gb = dO + bh * st.o_sbh;
+  const float *lse_b = lse + (long long)bh * Lq;
+  const float *dl_b = delta + (long long)bh * Lq;
+  const float sl2 = scale * kLog2e;
+  f32x16 Y1[D / 32], Y2[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) {
+    Y1[db] = f32x16{};
+    Y2[db] = f32x16{};
+  }
+  typename C::Regs qr, gr;
+  float lr = INFINITY, dr = 0.f;
+  fwd2_load<D, NW>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, 0, Lq);
+  if (threadIdx.x < kKT) {
+    lr = threadIdx.x < Lq ? lse_b[threadIdx.x] * kLog2e : INFINITY;
+    dr = threadIdx.x < Lq ? dl_b[threadIdx.x] : 0.f;
+  }
+  fwd2_store<D, NW>(sq, sg, qr, gr);
+  if (threadIdx.x < kKT) {
+    slse[threadIdx.x] = lr;
+    sdl[threadIdx.x] = dr;
+  }
+  lds_barrier();
+  const int ntiles = (Lq + kKT - 1) / kKT;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const int r0 = t * kKT;
+    if (t + 1 < ntiles) {
+      fwd2_load<D, NW>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, r0 + kKT, Lq);
+      if (threadIdx.x < kKT) {
+        const int q = r0 + kKT + threadIdx.x;
+        lr = q < Lq ? lse_b[q] * kLog2e : INFINITY;
+        dr = q < Lq ? dl_b[q] : 0.f;
+      }
+    }
+    const __bf16 *cq = sq + cur * C::kKBuf;
+    const __bf16 *cg = sg + cur * C::kVBuf;
+    const float *cl = slse + cur * kKT;
+    const float *cd = sdl + cur * kKT;
+    f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
+    k_product<D, C::kKS>(S0, cq, kf);                 // S  (queries x keys)
+    k_product<D, C::kKS>(S1, cq + 32 * C::kKS, kf);
+    k_product<D, C::kVS>(G0, cg, vf);                 // dP (queries x keys)
+    k_product<D, C::kVS>(G1, cg + 32 * C::kVS, vf);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = acc_row(r, h);
+      const float p0 = exp2f(__builtin_fmaf(S0[r], sl2, -cl[row]));  // 0 for rows beyond Lq (lse = +inf)
+      const float p1 = exp2f(__builtin_fmaf(S1[r], sl2, -cl[row + 32]));
+      S0[r] = p0;
+      S1[r] = p1;
+      G0[r] = p0 * (G0[r] - cd[row]);
+      G1[r] = p1 * (G1[r] - cd[row + 32]);
+    }
+    v_product<D, C::kVS>(Y1, cg, S0);  // dV^T += dO^T P
+    v_product<D, C::kVS>(Y1, cg + 32 * C::kVS, S1);
+    v_product<D, C::kKS>(Y2, cq, G0);  // dK^T += Q^T dS
+    v_product<D, C::kKS>(Y2, cq + 32 * C::kKS, G1);
+    if (t + 1 < ntiles) {
+      fwd2_store<D, NW>(sq + (cur ^ 1) * C::kKBuf, sg + (cur ^ 1) * C::kVBuf, qr, gr);
+      if (threadIdx.x < kKT) {
+        slse[(cur ^ 1) * kKT + threadIdx.x] = lr;
+        sdl[(cur ^ 1) * kKT + threadIdx.x] = dr;
+      }
+    }
+    lds_barrier();
+  }
+  store_Y<__bf16, D>(Y1, dV + bh * st.v_sbh, st.v_srow, k0w, Lk, 1.f);
+  store_Y<__bf16, D>(Y2, dK + bh * st.k_sbh, st.k_srow, k0w, Lk, scale);
+}
+
+template <int D, int NW>
+int launch_dq2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+               void *dq, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
+  using C = Fwd2Cfg<D, NW>;
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
+  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
+  const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
+  hipLaunchKernelGGL((attn_dq2_kernel<D, NW>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dq, Lq, Lk,
+                     scale, st);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+template <int D, int NW>
+int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+                void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
+  using C = Fwd2Cfg<D, NW>;
+  const size_t lds = C::kLds + 4 * kKT * sizeof(float);
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
+  const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
+  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q, (const __bf16 *)k,
+                     (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk, (__bf16 *)dv, Lq, Lk, scale,
+                     st);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+int dq2_dispatch(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+                 void *dq, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s) {
+  const bool wide = Lq > 128;
+  switch (D) {
+    case 32:
+      return wide ? launch_dq2<32, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s)
+                  : launch_dq2<32, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+    case 64:
+      return wide ? launch_dq2<64, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s)
+                  : launch_dq2<64, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+    case 96:
+      return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+    case 128:
+      return launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+    default:
+      return PCOPS_ERR_UNSUPPORTED;
+  }
+}
+
+int dkv2_dispatch(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+                  void *dk, void *dv, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s) {
+  const bool wide = Lk > 128;
+  switch (D) {
+    case 32:
+      return wide ? launch_dkv2<32, 8>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s)
+                  : launch_dkv2<32, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+    case 64:
+      return wide ? launch_dkv2<64, 8>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s)
+                  : launch_dkv2<64, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+    case 96:
+      return launch_dkv2<96, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+    case 128:
+      return launch_dkv2<128, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+    default:
+      return PCOPS_ERR_UNSUPPORTED;
+  }
+}
+
+int fwd2_dispatch(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, int D,
+                  float scale, const Strides &st, hipStream_t s) {
+  const bool wide = Lq > 128;
+  switch (D) {
+    case 32:
+      return wide ? launch_fwd2<32, 8>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s)
+                  : launch_fwd2<32, 4>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+    case 64:
+      return wide ? launch_fwd2<64, 8>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s)
+                  : launch_fwd2<64, 4>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+    case 96:
+      return wide ? launch_fwd2<96, 8>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s)
+                  : launch_fwd2<96, 4>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+    case 128:
+      return wide ? launch_fwd2<128, 8>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s)
+                  : launch_fwd2<128, 4>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+    default:
+      return PCOPS_ERR_UNSUPPORTED;
+  }
+}
+
+bool use_v1() {
+  static const int v = [] {
+    const char *e = getenv("PCOPS_ATTN_V1");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 bool aligned_ok(const void *p, long long s_bh, long long s_row, int esize) {
   const int vec = 16 / esize;
   return ((uintptr_t)p % 16 == 0) && (s_bh % vec == 0) && (s_row % vec == 0);
@@ -460,8 +918,9 @@ extern "C" int pcops_attention_forward(const void *q, const void *k, const void 
     return PCOPS_ERR_UNSUPPORTED;
   const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
   hipStream_t s = (hipStream_t)stream;
-  return dtype == 0 ? launch_fwd<float>(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s)
-                    : launch_fwd<__bf16>(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s);
+  if (dtype == 0) return launch_fwd<float>(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s);
+  if (use_v1()) return launch_fwd<__bf16>(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s);
+  return fwd2_dispatch(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s);
 }
 
 extern "C" unsigned long long pcops_attention_bwd_workspace_bytes(int BH, int Lq, int Lk, int D) {
@@ -503,8 +962,9 @@ extern "C" int pcops_attention_bwd_dq(const void *q, const void *k, const void *
   const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
   hipStream_t s = (hipStream_t)stream;
   const float *delta = (const float *)workspace;
-  return dtype == 0 ? launch_dq<float>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s)
-                    : launch_dq<__bf16>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s);
+  if (dtype == 0) return launch_dq<float>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s);
+  if (use_v1()) return launch_dq<__bf16>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s);
+  return dq2_dispatch(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s);
 }
 
 extern "C" int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const void *dout,
@@ -525,8 +985,9 @@ extern "C" int pcops_attention_bwd_dkv(const void *q, const void *k, const void 
   const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
   hipStream_t s = (hipStream_t)stream;
   const float *delta = (const float *)workspace;
-  return dtype == 0 ? launch_dkv<float>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s)
-                    : launch_dkv<__bf16>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
+  if (dtype == 0) return launch_dkv<float>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
+  if (use_v1()) return launch_dkv<__bf16>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
+  return dkv2_dispatch(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
 }
 
 // dq/dk/dv use the q/k/v strides; dout uses the o strides.

@@ -14,8 +14,6 @@
 
 namespace {
 
-constexpr int kThreads = 256;
-
 // torch CPU sum-of-squares order (oracle_torch_sumsq): C%32==0 (<=512) ->
 // four 8-lane accumulators over 32-element chunks; otherwise sequential.
 __device__ __forceinline__ float torch_sumsq(const float *v, int C) {
@@ -78,15 +76,74 @@ __device__ __forceinline__ void topk_store(const float (&bd)[KK], const int (&bi
   }
 }
 
+// Block = 64 queries x G waves.  Wave w scans its own slice of every LDS
+// candidate tile (ascending index inside the slice), so each (query, wave)
+// keeps a sorted top-KK of a candidate subset; the G lists are then merged in
+// LDS by wave 0 in lexicographic (distance, index) order -- the same total
+// order the single-list scan produces.  G > 1 multiplies the waves in flight
+// (the small-S calls would otherwise occupy a handful of CUs).
+template <int KK, int G>
+struct MergeBuf {
+  float d[G][KK][64];
+  int i[G][KK][64];
+};
+
+template <int KK, int G>
+__device__ __forceinline__ void merge_and_store(MergeBuf<KK, G> &mb, const float (&bd)[KK], const int (&bi)[KK],
+                                                int w, int lane, bool valid, int K, int pad, int n_avail,
+                                                int *out_idx, float *out_dist) {
+  if (G == 1) {
+    if (valid) topk_store<KK>(bd, bi, K, pad, n_avail, out_idx, out_dist);
+    return;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    mb.d[w][k][lane] = bd[k];
+    mb.i[w][k][lane] = bi[k];
+  }
+  __syncthreads();
+  if (w != 0 || !valid) return;
+  int head[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) head[g] = 0;
+  const int need = min(KK, K + pad);
+  for (int o = 0; o < need; ++o) {
+    float bdv = INFINITY;
+    int biv = INT_MAX, bw = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (head[g] < KK) {
+        const float dv = mb.d[g][head[g]][lane];
+        const int iv = mb.i[g][head[g]][lane];
+        if (dv < bdv || (dv == bdv && iv < biv)) {
+          bdv = dv;
+          biv = iv;
+          bw = g;
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) head[g] += (g == bw);
+    if (o >= pad) {
+      const bool ok = o < n_avail;
+      out_idx[o - pad] = ok ? biv : 0;
+      if (out_dist) out_dist[o - pad] = ok ? bdv : 0.f;
+    }
+  }
+}
+
 // C == 3: candidates staged as float4 (x, y, z, |p|^2)
-template <int KK>
-__global__ __launch_bounds__(kThreads) void knn3_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
-                                                        int N, int K, int pad, int *__restrict__ idx,
-                                                        float *__restrict__ dist) {
-  constexpr int TN = 1024;
+template <int KK, int G>
+__global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
+                                                      int N, int K, int pad, int *__restrict__ idx,
+                                                      float *__restrict__ dist) {
+  constexpr int TN = 1024, SL = TN / G;
   __shared__ float4 tile[TN];
+  __shared__ MergeBuf<KK, G> mb;
   const int b = blockIdx.y;
-  const int s = blockIdx.x * kThreads + threadIdx.x;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 64 + lane;
   const float *qb = q + (size_t)b * S * 3;
   const float *pb = p + (size_t)b * N * 3;
   const int sc = s < S ? s : S - 1;
@@ -102,13 +159,14 @@ __global__ __launch_bounds__(kThreads) void knn3_kernel(const float *__restrict_
   }
   for (int t0 = 0; t0 < N; t0 += TN) {
     const int cnt = min(TN, N - t0);
-    for (int e = threadIdx.x; e < cnt; e += kThreads) {
+    for (int e = threadIdx.x; e < cnt; e += 64 * G) {
       const float *src = pb + (size_t)(t0 + e) * 3;
       const float x = src[0], y = src[1], z = src[2];
       tile[e] = make_float4(x, y, z, (x * x + y * y) + z * z);
     }
     __syncthreads();
-    for (int e = 0; e < cnt; ++e) {
+    const int e1 = min(cnt, (w + 1) * SL);
+    for (int e = w * SL; e < e1; ++e) {
       const float4 c = tile[e];
       const float dot = __builtin_fmaf(mz, c.z, __builtin_fmaf(my, c.y, mx * c.x));
       const float d = (dot + qn) + c.w;
@@ -116,22 +174,26 @@ __global__ __launch_bounds__(kThreads) void knn3_kernel(const float *__restrict_
     }
     __syncthreads();
   }
-  if (s < S) topk_store<KK>(bd, bi, K, pad, N, idx + ((size_t)b * S + s) * K, dist ? dist + ((size_t)b * S + s) * K : nullptr);
+  merge_and_store<KK, G>(mb, bd, bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
+                         dist ? dist + ((size_t)b * S + sc) * K : nullptr);
 }
 
 // generic C (feature space): candidates staged 32 at a time (32 x C floats),
-// query channels read in 32-wide chunks; the per-candidate dot keeps the
-// sequential channel order across chunks.
-template <int KK>
-__global__ __launch_bounds__(kThreads) void knnC_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
-                                                        int N, int C, int K, int pad, int *__restrict__ idx,
-                                                        float *__restrict__ dist) {
+// wave w takes candidates [w*32/G, (w+1)*32/G) of each tile; query channels
+// read in 32-wide chunks, the per-candidate dot keeps the sequential channel
+// order across chunks.
+template <int KK, int G>
+__global__ __launch_bounds__(64 * G) void knnC_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
+                                                      int N, int C, int K, int pad, int *__restrict__ idx,
+                                                      float *__restrict__ dist) {
   extern __shared__ __attribute__((aligned(16))) float smem[];  // [32][C] candidates + [32] norms
-  constexpr int TN = 32;
+  constexpr int TN = 32, PW = TN / G;
+  __shared__ MergeBuf<KK, G> mb;
   float *tc = smem;
   float *tn = smem + TN * C;
   const int b = blockIdx.y;
-  const int s = blockIdx.x * kThreads + threadIdx.x;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 64 + lane;
   const float *qb = q + (size_t)b * S * C;
   const float *pb = p + (size_t)b * N * C;
   const int sc = s < S ? s : S - 1;
@@ -146,15 +208,16 @@ __global__ __launch_bounds__(kThreads) void knnC_kernel(const float *__restrict_
   }
   for (int t0 = 0; t0 < N; t0 += TN) {
     const int cnt = min(TN, N - t0);
-    for (int e = threadIdx.x; e < TN * C; e += kThreads) {
+    for (int e = threadIdx.x; e < TN * C; e += 64 * G) {
       const int kk = e / C;
       tc[e] = kk < cnt ? pb[(size_t)t0 * C + e] : 0.f;
     }
     __syncthreads();
     if (threadIdx.x < cnt) tn[threadIdx.x] = torch_sumsq(tc + threadIdx.x * C, C);
-    float dot[TN];
+    float dot[PW];
 #pragma unroll
-    for (int k = 0; k < TN; ++k) dot[k] = 0.f;
+    for (int k = 0; k < PW; ++k) dot[k] = 0.f;
+    const float *tw = tc + w * PW * C;
     for (int c0 = 0; c0 < C; c0 += 32) {
       const int cw = min(32, C - c0);
       float qc[32];
@@ -162,37 +225,41 @@ __global__ __launch_bounds__(kThreads) void knnC_kernel(const float *__restrict_
       for (int c = 0; c < 32; ++c) qc[c] = c < cw ? qq[c0 + c] : 0.f;
       if (cw == 32) {
 #pragma unroll
-        for (int k = 0; k < TN; ++k) {
-          const float *pc = tc + k * C + c0;
+        for (int k = 0; k < PW; ++k) {
+          const float *pc = tw + k * C + c0;
 #pragma unroll
           for (int c = 0; c < 32; ++c) dot[k] = __builtin_fmaf(qc[c], pc[c], dot[k]);
         }
       } else {
 #pragma unroll
-        for (int k = 0; k < TN; ++k) {
-          const float *pc = tc + k * C + c0;
+        for (int k = 0; k < PW; ++k) {
+          const float *pc = tw + k * C + c0;
           for (int c = 0; c < cw; ++c) dot[k] = __builtin_fmaf(qc[c], pc[c], dot[k]);
         }
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < TN; ++k)
-      if (k < cnt) topk_insert<KK>(bd, bi, ((-2.f * dot[k]) + qn) + tn[k], t0 + k);
+    for (int k = 0; k < PW; ++k) {
+      const int e = w * PW + k;
+      if (e < cnt) topk_insert<KK>(bd, bi, ((-2.f * dot[k]) + qn) + tn[e], t0 + e);
+    }
     __syncthreads();
   }
-  if (s < S) topk_store<KK>(bd, bi, K, pad, N, idx + ((size_t)b * S + s) * K, dist ? dist + ((size_t)b * S + s) * K : nullptr);
+  merge_and_store<KK, G>(mb, bd, bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
+                         dist ? dist + ((size_t)b * S + sc) * K : nullptr);
 }
 
 template <int KK>
 int launch_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
                hipStream_t st) {
-  const dim3 grid((S + kThreads - 1) / kThreads, B);
+  constexpr int G = KK <= 16 ? 4 : (KK <= 32 ? 2 : 1);
+  const dim3 grid((S + 63) / 64, B);
   if (C == 3) {
-    hipLaunchKernelGGL(knn3_kernel<KK>, grid, dim3(kThreads), 0, st, q, p, S, N, K, pad, idx, dist);
+    hipLaunchKernelGGL((knn3_kernel<KK, G>), grid, dim3(64 * G), 0, st, q, p, S, N, K, pad, idx, dist);
   } else {
     const size_t lds = sizeof(float) * (32 * (size_t)C + 32);
-    hipLaunchKernelGGL(knnC_kernel<KK>, grid, dim3(kThreads), lds, st, q, p, S, N, C, K, pad, idx, dist);
+    hipLaunchKernelGGL((knnC_kernel<KK, G>), grid, dim3(64 * G), lds, st, q, p, S, N, C, K, pad, idx, dist);
   }
   PC_CHECK_LAUNCH();
   return PCOPS_OK;

@@ -1,0 +1,38 @@
+"""Attention core timing at the PCN shapes (B=32), forward and backward,
+per libpcops launch (HIP events via _lib.KernelTimer).  PCOPS_ATTN_V1=1 in
+the environment selects the first-generation kernels for A/B runs."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from svdformer_pointsea_amd import _lib
+from svdformer_pointsea_amd.attention import attention_core
+
+torch.manual_seed(0)
+B = 32
+shapes = [  # (Lq, Lk, E, H) seen in the PCN step
+    (2048, 2048, 512, 8), (2048, 2048, 1024, 8), (2048, 512, 512, 8), (512, 512, 768, 8), (512, 512, 512, 8),
+    (128, 128, 512, 4)]
+tag = "v1" if os.environ.get("PCOPS_ATTN_V1") == "1" else "v2"
+for Lq, Lk, E, H in shapes:
+    q = torch.randn(Lq, B, E, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(Lk, B, E, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(Lk, B, E, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(Lq, B, E, device="cuda", dtype=torch.bfloat16)
+    for _ in range(3):
+        attention_core(q, k, v, H).backward(g)
+    torch.cuda.synchronize()
+    _lib.KernelTimer.enable()
+    for _ in range(10):
+        attention_core(q, k, v, H).backward(g)
+    torch.cuda.synchronize()
+    summ = _lib.KernelTimer.summary()
+    _lib.KernelTimer.disable()
+    hd = E // H
+    fl = 4.0 * B * H * Lq * Lk * hd
+    out = []
+    for name, mult in [("attention forward", 1), ("attention bwd dq", 0.5), ("attention bwd dkv", 2.0),
+                       ("attention bwd delta", 0)]:
+        n, mean, tot = summ[name]
+        tf = fl * mult / (mean * 1e-3) / 1e12 if mult else 0
+        out.append(f"{name.split()[-1]} {mean:.3f}ms {tf:.0f}TF")
+    print(f"{tag} Lq={Lq} Lk={Lk} E={E} H={H} hd={hd}: " + " | ".join(out), flush=True)
