@@ -119,41 +119,70 @@ int pcops_emd_backward(const float *xyz1, const float *xyz2, const float *graddi
 
 /* ---------------- attention core (nn.MultiheadAttention inside
  * self_attention / cross_attention, models/model_utils.py:542-617) ----------------
- * O = softmax(scale * Q K^T) V per (batch*head), flash-style (no L x L
- * matrix in HBM).  Tensors are addressed as base + bh*s_bh + row*s_row + d
- * (elements), so the seq-first (L, B*H, hd) layout of MultiheadAttention is
- * used in place.  dtype 0 = fp32 (f32 MFMA, parity build), 1 = bf16 in/out
- * with fp32 accumulation.  lse (BH, Lq) fp32 log-sum-exp (natural log) for
- * the backward.  head_dim in {32, 64, 96, 128}. */
-int pcops_attention_forward(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk,
-                            int D, float scale, int dtype, long long q_sbh, long long q_srow, long long k_sbh,
-                            long long k_srow, long long v_sbh, long long v_srow, long long o_sbh, long long o_srow,
-                            pcops_stream_t stream);
-/* dQ, dK, dV (dtype as forward; dq/dk/dv overwritten).  workspace:
- * pcops_attention_bwd_workspace_bytes(BH, Lq, Lk, D). */
-unsigned long long pcops_attention_bwd_workspace_bytes(int BH, int Lq, int Lk, int D);
+ * O = softmax(scale * Q K^T) V per (batch, head), flash-style (no L x L
+ * matrix in HBM).  Element (b, h, row, d) of each tensor is read at
+ * base + b*sb + h*sh + row*srow + d (elements), so nn.MultiheadAttention's
+ * seq-first (L, B, H*hd) projections [sb = H*hd, sh = hd, srow = B*H*hd] and
+ * batch-first (B, L, H*hd) tensors [sb = L*H*hd, sh = hd, srow = H*hd] are used
+ * in place.  dtype 0 = fp32 (exact f32 MFMA, parity build), 1 = bf16 in/out
+ * with fp32 accumulation.  lse (B*H, Lq) fp32 log-sum-exp (natural log) for
+ * the backward.  head_dim D in {32, 64, 96, 128}; pointers and strides must be
+ * 16-byte aligned (else PCOPS_ERR_UNSUPPORTED). */
+int pcops_attention_forward(const void *q, const void *k, const void *v, void *o, float *lse, int B, int H, int Lq,
+                            int Lk, int D, float scale, int dtype, long long q_sb, long long q_sh, long long q_srow,
+                            long long k_sb, long long k_sh, long long k_srow, long long v_sb, long long v_sh,
+                            long long v_srow, long long o_sb, long long o_sh, long long o_srow, pcops_stream_t stream);
+/* Backward of the above (dq/dk/dv use the q/k/v strides, dout the o strides).
+ * workspace: pcops_attention_bwd_workspace_bytes(B, H, Lq, Lk, D). */
+unsigned long long pcops_attention_bwd_workspace_bytes(int B, int H, int Lq, int Lk, int D);
 int pcops_attention_backward(const void *q, const void *k, const void *v, const void *o, const void *dout,
-                             const float *lse, void *dq, void *dk, void *dv, int BH, int Lq, int Lk, int D,
-                             float scale, int dtype, long long q_sbh, long long q_srow, long long k_sbh,
-                             long long k_srow, long long v_sbh, long long v_srow, long long o_sbh, long long o_srow,
-                             void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
-
+                             const float *lse, void *dq, void *dk, void *dv, int B, int H, int Lq, int Lk, int D,
+                             float scale, int dtype, long long q_sb, long long q_sh, long long q_srow, long long k_sb,
+                             long long k_sh, long long k_srow, long long v_sb, long long v_sh, long long v_srow,
+                             long long o_sb, long long o_sh, long long o_srow, void *workspace,
+                             unsigned long long workspace_bytes, pcops_stream_t stream);
 /* The three launches of pcops_attention_backward, exposed separately so a
  * caller can time or overlap them: delta = rowsum(dO o O) into workspace,
  * then dQ (query-on-lane pass), then dK/dV (key-on-lane pass). */
-int pcops_attention_bwd_preprocess(const void *o, const void *dout, int BH, int Lq, int D, int dtype, long long o_sbh,
-                                   long long o_srow, void *workspace, unsigned long long workspace_bytes,
-                                   pcops_stream_t stream);
+int pcops_attention_bwd_preprocess(const void *o, const void *dout, int B, int H, int Lq, int D, int dtype,
+                                   long long o_sb, long long o_sh, long long o_srow, void *workspace,
+                                   unsigned long long workspace_bytes, pcops_stream_t stream);
 int pcops_attention_bwd_dq(const void *q, const void *k, const void *v, const void *dout, const float *lse,
-                           void *dq, int BH, int Lq, int Lk, int D, float scale, int dtype, long long q_sbh,
-                           long long q_srow, long long k_sbh, long long k_srow, long long v_sbh, long long v_srow,
-                           long long o_sbh, long long o_srow, const void *workspace, unsigned long long workspace_bytes,
+                           void *dq, int B, int H, int Lq, int Lk, int D, float scale, int dtype, long long q_sb,
+                           long long q_sh, long long q_srow, long long k_sb, long long k_sh, long long k_srow,
+                           long long v_sb, long long v_sh, long long v_srow, long long o_sb, long long o_sh,
+                           long long o_srow, const void *workspace, unsigned long long workspace_bytes,
                            pcops_stream_t stream);
 int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const void *dout, const float *lse,
-                            void *dk, void *dv, int BH, int Lq, int Lk, int D, float scale, int dtype,
-                            long long q_sbh, long long q_srow, long long k_sbh, long long k_srow, long long v_sbh,
-                            long long v_srow, long long o_sbh, long long o_srow, const void *workspace,
+                            void *dk, void *dv, int B, int H, int Lq, int Lk, int D, float scale, int dtype,
+                            long long q_sb, long long q_sh, long long q_srow, long long k_sb, long long k_sh,
+                            long long k_srow, long long v_sb, long long v_sh, long long v_srow, long long o_sb,
+                            long long o_sh, long long o_srow, const void *workspace,
                             unsigned long long workspace_bytes, pcops_stream_t stream);
+
+/* ---------------- attention-block glue (self_attention / cross_attention,
+ * models/model_utils.py:584-617 and :542-582: the permute(2,0,1) / permute(1,2,0)
+ * layout changes, `src1 + src12`, norm13 / norm12 LayerNorms) ----------------
+ * dtype codes: 0 = fp32, 1 = bf16.  Rows are C contiguous elements.
+ * pcops_transpose_add: out[b][c][r] = a[b][r][c] (+ b[b][r][c] when b != NULL);
+ *   out2 (optional) receives the same values in out2_dtype. */
+int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype, void *out2,
+                        int out2_dtype, int B, int R, int C, pcops_stream_t stream);
+/* pcops_layernorm_fwd: x = a (+ b); y = (x - mean) * rstd * gamma + beta per row
+ * (torch.nn.LayerNorm over the last dim), written as fp32 (y32) and/or bf16
+ * (y16); mean / rstd (rows) saved for the backward.  C <= 1024, C % 8 == 0,
+ * rows 16-byte aligned. */
+int pcops_layernorm_fwd(const void *a, int a_dtype, const void *b, int b_dtype, const float *gamma, const float *beta,
+                        float eps, int rows, int C, float *y32, void *y16, float *mean, float *rstd,
+                        pcops_stream_t stream);
+/* pcops_layernorm_bwd: dy = dy32 + dy16 (either may be NULL); dx written as
+ * fp32 (dx32) and/or bf16 (dx16) -- the gradient of both a and b; dgamma /
+ * dbeta (C) are overwritten.  workspace: pcops_layernorm_bwd_workspace_bytes. */
+unsigned long long pcops_layernorm_bwd_workspace_bytes(int rows, int C);
+int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b, int b_dtype,
+                        const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
+                        void *dx16, float *dgamma, float *dbeta, void *workspace, unsigned long long workspace_bytes,
+                        pcops_stream_t stream);
 
 /* ---------------- depth renderers ----------------
  * PCViews.get_img (models/model_utils.py:1196-1234 -> points2depth :1080-1115 ->

@@ -10,8 +10,8 @@ a `with cpu_ops():` block, for:
 
   * the C restatement in oracle/pcops_oracle.c (FPS, gather, group, kNN,
     Chamfer, depth splat) -- single-threaded C, as the checker is;
-  * torch CPU math for the attention core (what nn.MultiheadAttention does
-    on CPU in the reference).
+  * torch CPU math for the attention core and the attention blocks' fused
+    LayerNorm / transpose glue (what the reference's torch modules do on CPU).
 
 Everything else (convolutions, LayerNorm, Adam) is torch on CPU threads.
 The product package never imports this module; outside the `with` block the
@@ -92,18 +92,39 @@ def _knn(q, p, k, pad=0, want_dist=False):
 
 
 class _AttentionCore:
-    """softmax(scale q k^T) v on seq-first (L, B, E) tensors, torch CPU math."""
+    """softmax(scale q k^T) v, torch CPU math, same (meta, *srcs) calling
+    convention as svdformer_pointsea_amd.attention.AttentionCore."""
 
     @staticmethod
-    def apply(q, k, v, heads, scale):
-        Lq, B, E = q.shape
+    def apply(meta, *srcs):
+        heads, scale, E, bf, qw, kw, vw = meta
+        q, k, v = (srcs[w[0]][..., w[1]:w[1] + E] for w in (qw, kw, vw))
+        if bf:  # (B, L, E) -> (L, B, E)
+            q, k, v = (t.transpose(0, 1) for t in (q, k, v))
+        Lq, B, _ = q.shape
         Lk = k.shape[0]
         hd = E // heads
         qh = q.reshape(Lq, B * heads, hd).transpose(0, 1)
         kh = k.reshape(Lk, B * heads, hd).transpose(0, 1)
         vh = v.reshape(Lk, B * heads, hd).transpose(0, 1)
         p = torch.softmax(torch.bmm(qh * scale, kh.transpose(1, 2)), dim=-1)
-        return torch.bmm(p, vh).transpose(0, 1).reshape(Lq, B, E)
+        o = torch.bmm(p, vh).transpose(0, 1).reshape(Lq, B, E)
+        return o.transpose(0, 1).contiguous() if bf else o
+
+
+class _TransposeAdd:
+    @staticmethod
+    def apply(a, b, out_dtype):
+        x = a if b is None else a + b
+        return x.transpose(1, 2).contiguous().to(out_dtype)
+
+
+class _LayerNorm:
+    @staticmethod
+    def apply(a, b, weight, bias, eps, want16):
+        x = (a if b is None else a + b).float()
+        y = torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+        return (y, y.to(torch.bfloat16)) if want16 else y
 
 
 def depth_images(render, points):
@@ -129,6 +150,8 @@ def cpu_ops():
         (svdformer, "gather_operation", _Gather.apply),
         (chamfer3D, "chamfer_3DFunction", _Chamfer),
         (attention, "AttentionCore", _AttentionCore),
+        (attention, "_TransposeAdd", _TransposeAdd),
+        (attention, "_LayerNorm", _LayerNorm),
     ]
     saved = [(m, n, getattr(m, n)) for m, n, _ in patches]
     try:

@@ -40,14 +40,16 @@ _SIGS = {
     "pcops_emd_workspace_bytes": (ULL, [I, I]),
     "pcops_emd_forward": (I, [P, P, I, I, F, I, P, P, P, ULL, P]),
     "pcops_emd_backward": (I, [P, P, P, P, I, I, P, P]),
-    "pcops_attention_forward": (I, [P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P]),
-    "pcops_attention_bwd_workspace_bytes": (ULL, [I, I, I, I]),
-    "pcops_attention_backward": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P,
-                                     ULL, P]),
-    "pcops_attention_bwd_preprocess": (I, [P, P, I, I, I, I, LL, LL, P, ULL, P]),
-    "pcops_attention_bwd_dq": (I, [P, P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
-    "pcops_attention_bwd_dkv": (I, [P, P, P, P, P, P, P, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL,
-                                    P]),
+    "pcops_attention_forward": (I, [P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P]),
+    "pcops_attention_bwd_workspace_bytes": (ULL, [I, I, I, I, I]),
+    "pcops_attention_backward": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
+    "pcops_attention_bwd_preprocess": (I, [P, P, I, I, I, I, I, LL, LL, LL, P, ULL, P]),
+    "pcops_attention_bwd_dq": (I, [P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
+    "pcops_attention_bwd_dkv": (I, [P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
+    "pcops_transpose_add": (I, [P, I, P, I, P, I, P, I, I, I, I, P]),
+    "pcops_layernorm_fwd": (I, [P, I, P, I, P, P, F, I, I, P, P, P, P, P]),
+    "pcops_layernorm_bwd_workspace_bytes": (ULL, [I, I]),
+    "pcops_layernorm_bwd": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, ULL, P]),
     "pcops_points2depth_workspace_bytes": (ULL, [I, I, I, I]),
     "pcops_points2depth": (I, [P, P, P, I, I, I, I, I, P, P, ULL, P]),
     "pcops_points2grid": (I, [P, P, P, P, I, I, I, I, I, P, P]),
@@ -134,7 +136,8 @@ def call(what, fn, *args):
     e0.record(s)
     status = fn(*args)
     e1.record(s)
-    scalars = tuple(a if isinstance(a, (int, float)) else None for a in args)
+    # sizes as given; pointers as their address (None for NULL)
+    scalars = tuple(a if isinstance(a, (int, float)) else (a.value if isinstance(a, P) else None) for a in args)
     spans.setdefault(what, []).append((e0, e1, scalars))
     check(status, what)
 

@@ -1,15 +1,24 @@
 """Attention blocks of models/model_utils.py (:542-629) and
-models_PointSea/model_utils.py (:385-509) with the attention core
-(softmax(QK^T/sqrt(hd)) V, forward and backward) on libpcops.so MFMA kernels.
+models_PointSea/model_utils.py (:385-509) on libpcops.so.
 
 Parameter names match the reference exactly (multihead_attn.in_proj_weight,
 multihead_attn.out_proj.weight, linear11, linear12, norm12, norm13,
-input_proj, ...) so reference state_dicts load unchanged.  The projections,
-LayerNorms, GELU and residuals are the same torch ops the reference uses; only
-the O(L^2) part is replaced.  The core reads the seq-first (L, B, E) projection
-outputs in place (stride tricks, no transposes) and runs in fp32 (exact f32
-MFMA, parity build) or bf16 (bf16 MFMA, fp32 accumulation) following the
-dtype of its inputs (e.g. under torch.autocast).
+input_proj, ...), so reference state_dicts load unchanged, and every block
+keeps the reference's call signature: (B, C_in, L) in, (B, C_out, L) out.
+
+Inside, a block runs token-major (B, L, C) -- the MI355X layout for it:
+  * input_proj is a plain GEMM on the transposed input (the transpose is one
+    LDS-tiled pass, csrc/blockops.hip, instead of permute + .contiguous());
+  * norm13 / norm12 (with the residual add folded in) are one-pass fused
+    LayerNorms that also emit the bf16 copy the next GEMM reads under
+    autocast (no separate cast kernels);
+  * the q/k/v projections stay packed: the attention core reads q, k and v as
+    column windows of the projection output and writes dq/dk/dv into one
+    packed gradient (no chunk / cat copies);
+  * the output leaves through one fused add + transpose pass.
+The attention core (softmax(QK^T/sqrt(hd)) V, forward and backward) is the
+flash-style MFMA kernel: fp32 (exact f32 MFMA, the parity build) or bf16
+(fp32 accumulate) following the dtype of its inputs (e.g. torch.autocast).
 """
 import math
 
@@ -24,80 +33,127 @@ from ._lib import call, lib, ptr, stream_of
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
-def _strides(t, heads):
-    # t: (L, B, E) contiguous seq-first -> element (bh, row, d) at bh*hd + row*B*E + d
-    L, B, E = t.shape
-    return E // heads, B * E
+def _dt(t):
+    if t.dtype not in _DT:
+        raise RuntimeError(f"unsupported dtype {t.dtype}")
+    return _DT[t.dtype]
+
+
+def _vptr(t, off=0):
+    import ctypes
+
+    return ctypes.c_void_p(t.data_ptr() + off * t.element_size())
+
+
+# ------------------------------------------------------------------ attention core
+def _layout(t, batch_first):
+    """(sb, srow) element strides of a (B, L, W) / (L, B, W) tensor."""
+    return (t.stride(0), t.stride(1)) if batch_first else (t.stride(1), t.stride(0))
 
 
 class AttentionCore(Function):
-    """o = softmax(scale * q k^T) v per head; q (Lq,B,E), k/v (Lk,B,E) seq-first."""
+    """o = softmax(scale q k^T) v per head.
+
+    q, k and v are the column windows [off, off + E) of one to three distinct
+    source tensors (meta = (heads, scale, E, batch_first, (src, off) x 3)), so
+    packed projection outputs are read in place and their gradients written
+    in place."""
 
     @staticmethod
-    def forward(ctx, q, k, v, heads, scale):
-        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-        if not (q.is_cuda and k.is_cuda and v.is_cuda):
-            raise RuntimeError("attention core: tensors must be CUDA tensors")
-        if q.dtype not in _DT or k.dtype != q.dtype or v.dtype != q.dtype:
-            raise RuntimeError(f"attention core: unsupported dtype {q.dtype}")
-        Lq, B, E = q.shape
-        Lk = k.shape[0]
+    def forward(ctx, meta, *srcs):
+        heads, scale, E, bf, qw, kw, vw = meta
+        srcs = tuple(s.contiguous() for s in srcs)
+        for s in srcs:
+            if not s.is_cuda:
+                raise RuntimeError("attention core: tensors must be CUDA tensors")
+            if s.dtype not in _DT or s.dtype != srcs[0].dtype:
+                raise RuntimeError(f"attention core: unsupported dtype {s.dtype}")
+        q_t, k_t, v_t = srcs[qw[0]], srcs[kw[0]], srcs[vw[0]]
+        if bf:
+            B, Lq = q_t.shape[:2]
+            Lk = k_t.shape[1]
+        else:
+            Lq, B = q_t.shape[:2]
+            Lk = k_t.shape[0]
         hd = E // heads
-        o = torch.empty_like(q)
-        lse = torch.empty(B * heads, Lq, dtype=torch.float32, device=q.device)
-        sq, rq = _strides(q, heads)
-        sk, rk = _strides(k, heads)
-        with torch.cuda.device(q.device):
-            call("attention forward", lib().pcops_attention_forward, ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse),
-                 B * heads, Lq, Lk, hd, float(scale), _DT[q.dtype], sq, rq, sk, rk, sk, rk, sq, rq, stream_of(q))
-        ctx.save_for_backward(q, k, v, o, lse)
-        ctx.heads, ctx.scale = heads, scale
+        o = torch.empty((B, Lq, E) if bf else (Lq, B, E), dtype=q_t.dtype, device=q_t.device)
+        lse = torch.empty(B * heads, Lq, dtype=torch.float32, device=q_t.device)
+        (qb, qr), (kb, kr), (vb, vr), (ob, orow) = (_layout(t, bf) for t in (q_t, k_t, v_t, o))
+        with torch.cuda.device(q_t.device):
+            call("attention forward", lib().pcops_attention_forward, _vptr(q_t, qw[1]), _vptr(k_t, kw[1]),
+                 _vptr(v_t, vw[1]), ptr(o), ptr(lse), B, heads, Lq, Lk, hd, float(scale), _DT[q_t.dtype], qb, hd, qr,
+                 kb, hd, kr, vb, hd, vr, ob, hd, orow, stream_of(q_t))
+        ctx.save_for_backward(*srcs, o, lse)
+        ctx.meta, ctx.dims = meta, (B, Lq, Lk, hd)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse = ctx.saved_tensors
-        heads, scale = ctx.heads, ctx.scale
-        do = do.contiguous().to(q.dtype)
-        Lq, B, E = q.shape
-        Lk = k.shape[0]
-        hd = E // heads
-        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        sq, rq = _strides(q, heads)
-        sk, rk = _strides(k, heads)
-        wsb = lib().pcops_attention_bwd_workspace_bytes(B * heads, Lq, Lk, hd)
-        ws = _lib.Workspace.get(q.device, wsb)
-        BH, dt = B * heads, _DT[q.dtype]
-        st = (sq, rq, sk, rk, sk, rk, sq, rq)
-        with torch.cuda.device(q.device):
-            stream = stream_of(q)
-            call("attention bwd delta", lib().pcops_attention_bwd_preprocess, ptr(o), ptr(do), BH, Lq, hd, dt, sq, rq,
-                 ptr(ws), wsb, stream)
-            call("attention bwd dq", lib().pcops_attention_bwd_dq, ptr(q), ptr(k), ptr(v), ptr(do), ptr(lse), ptr(dq),
-                 BH, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream)
-            call("attention bwd dkv", lib().pcops_attention_bwd_dkv, ptr(q), ptr(k), ptr(v), ptr(do), ptr(lse), ptr(dk),
-                 ptr(dv), BH, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream)
-        return dq, dk, dv, None, None
+        *srcs, o, lse = ctx.saved_tensors
+        heads, scale, E, bf, qw, kw, vw = ctx.meta
+        B, Lq, Lk, hd = ctx.dims
+        do = do.contiguous().to(o.dtype)
+        covered = [0] * len(srcs)
+        for w in (qw, kw, vw):
+            covered[w[0]] += E
+        grads = [torch.empty_like(s) if covered[i] == s.shape[-1] else torch.zeros_like(s)
+                 for i, s in enumerate(srcs)]
+        q_t, k_t, v_t = srcs[qw[0]], srcs[kw[0]], srcs[vw[0]]
+        (qb, qr), (kb, kr), (vb, vr), (ob, orow) = (_layout(t, bf) for t in (q_t, k_t, v_t, o))
+        st = (qb, hd, qr, kb, hd, kr, vb, hd, vr, ob, hd, orow)
+        dt = _DT[o.dtype]
+        wsb = lib().pcops_attention_bwd_workspace_bytes(B, heads, Lq, Lk, hd)
+        ws = _lib.Workspace.get(o.device, wsb)
+        qp, kp, vp = _vptr(q_t, qw[1]), _vptr(k_t, kw[1]), _vptr(v_t, vw[1])
+        with torch.cuda.device(o.device):
+            stream = stream_of(o)
+            call("attention bwd delta", lib().pcops_attention_bwd_preprocess, ptr(o), ptr(do), B, heads, Lq, hd, dt,
+                 ob, hd, orow, ptr(ws), wsb, stream)
+            call("attention bwd dq", lib().pcops_attention_bwd_dq, qp, kp, vp, ptr(do), ptr(lse),
+                 _vptr(grads[qw[0]], qw[1]), B, heads, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream)
+            call("attention bwd dkv", lib().pcops_attention_bwd_dkv, qp, kp, vp, ptr(do), ptr(lse),
+                 _vptr(grads[kw[0]], kw[1]), _vptr(grads[vw[0]], vw[1]), B, heads, Lq, Lk, hd, float(scale), dt,
+                 *st, ptr(ws), wsb, stream)
+        return (None, *grads)
 
 
-def attention_core(q, k, v, heads, scale=None):
+def _windows(q, k, v):
+    """Deduplicate the q/k/v sources -> (srcs, (src, 0) windows)."""
+    srcs, wins = [], []
+    for t in (q, k, v):
+        for i, s in enumerate(srcs):
+            if s is t:
+                wins.append((i, 0))
+                break
+        else:
+            srcs.append(t)
+            wins.append((len(srcs) - 1, 0))
+    return srcs, wins
+
+
+def attention_core(q, k, v, heads, scale=None, batch_first=False):
+    """softmax(q k^T * scale) v for (L, B, E) (or (B, L, E)) q / k / v."""
     E = q.shape[-1]
     if scale is None:
         scale = 1.0 / math.sqrt(E // heads)
-    return AttentionCore.apply(q, k, v, heads, scale)
+    srcs, wins = _windows(q, k, v)
+    return AttentionCore.apply((heads, scale, E, batch_first, *wins), *srcs)
 
 
 class MultiheadAttention(nn.Module):
     """nn.MultiheadAttention(embed_dim, num_heads) subset used by the reference:
-    seq-first inputs, no masks, dropout 0, returns (output, None)."""
+    no masks, dropout 0, returns (output, None); seq-first by default like
+    torch, batch_first=True for the token-major blocks.  The projections are
+    fused per distinct input (q = k = v -> one (.., 3E) GEMM; q = k -> (.., 2E)
+    + (.., E); k = v -> (.., E) + (.., 2E)) and handed to the core packed."""
 
-    def __init__(self, embed_dim, num_heads, dropout=0.0, bias=True):
+    def __init__(self, embed_dim, num_heads, dropout=0.0, bias=True, batch_first=False):
         super().__init__()
         if dropout != 0.0:
             raise NotImplementedError("attention dropout is not used by the reference models (dropout=0.0)")
         if embed_dim % num_heads:
             raise ValueError("embed_dim must be divisible by num_heads")
-        self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.embed_dim, self.num_heads, self.batch_first = embed_dim, num_heads, batch_first
         self.head_dim = embed_dim // num_heads
         self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
         self.in_proj_bias = nn.Parameter(torch.empty(3 * embed_dim)) if bias else None
@@ -110,136 +166,248 @@ class MultiheadAttention(nn.Module):
             nn.init.constant_(self.in_proj_bias, 0.0)
             nn.init.constant_(self.out_proj.bias, 0.0)
 
+    def _proj(self, x, r0, r1):
+        b = None if self.in_proj_bias is None else self.in_proj_bias[r0:r1]
+        return F.linear(x, self.in_proj_weight[r0:r1], b)
+
     def forward(self, query, key, value, need_weights=True):
-        E = self.embed_dim
-        w, b = self.in_proj_weight, self.in_proj_bias
-        bq, bk, bv = (None, None, None) if b is None else (b[:E], b[E:2 * E], b[2 * E:])
+        E, H = self.embed_dim, self.num_heads
+        scale = 1.0 / math.sqrt(self.head_dim)
         if query is key and key is value:
-            q, k, v = F.linear(query, w, b).chunk(3, dim=-1)
+            srcs = (self._proj(query, 0, 3 * E),)
+            wins = ((0, 0), (0, E), (0, 2 * E))
         elif query is key:
-            q, k = F.linear(query, w[:2 * E], None if b is None else b[:2 * E]).chunk(2, dim=-1)
-            v = F.linear(value, w[2 * E:], bv)
+            srcs = (self._proj(query, 0, 2 * E), self._proj(value, 2 * E, 3 * E))
+            wins = ((0, 0), (0, E), (1, 0))
+        elif key is value:
+            srcs = (self._proj(query, 0, E), self._proj(key, E, 3 * E))
+            wins = ((0, 0), (1, 0), (1, E))
         else:
-            q = F.linear(query, w[:E], bq)
-            if key is value:
-                k, v = F.linear(key, w[E:], None if b is None else b[E:]).chunk(2, dim=-1)
-            else:
-                k = F.linear(key, w[E:2 * E], bk)
-                v = F.linear(value, w[2 * E:], bv)
-        o = attention_core(q, k, v, self.num_heads)
+            srcs = (self._proj(query, 0, E), self._proj(key, E, 2 * E), self._proj(value, 2 * E, 3 * E))
+            wins = ((0, 0), (1, 0), (2, 0))
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
+        if dt is not None and any(s.dtype != dt for s in srcs):
+            srcs = tuple(s.to(dt) for s in srcs)
+        o = AttentionCore.apply((H, scale, E, self.batch_first, *wins), *srcs)
         return self.out_proj(o), None
 
 
-class self_attention(nn.Module):
+# ------------------------------------------------------------------ fused block glue
+def _cuda_only(what, *ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(f"{what}: tensors must be CUDA tensors")
+
+
+class _TransposeAdd(Function):
+    """(B, R, C) [+ (B, R, C)] -> (B, C, R) in `out_dtype`, one LDS-tiled pass."""
+
+    @staticmethod
+    def forward(ctx, a, b, out_dtype):
+        _cuda_only("transpose_add", a, b)
+        a = a.contiguous()
+        b = None if b is None else b.contiguous()
+        B, R, C = a.shape
+        out = torch.empty(B, C, R, dtype=out_dtype, device=a.device)
+        with torch.cuda.device(a.device):
+            call("transpose_add", lib().pcops_transpose_add, ptr(a), _dt(a), ptr(b), 0 if b is None else _dt(b),
+                 ptr(out), _DT[out_dtype], None, 0, B, R, C, stream_of(a))
+        ctx.dtypes = (a.dtype, None if b is None else b.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        B, C, R = g.shape
+        adt, bdt = ctx.dtypes
+        ga = torch.empty(B, R, C, dtype=adt, device=g.device)
+        gb = None if bdt is None else torch.empty(B, R, C, dtype=bdt, device=g.device)
+        with torch.cuda.device(g.device):
+            call("transpose_add", lib().pcops_transpose_add, ptr(g), _dt(g), None, 0, ptr(ga), _DT[adt], ptr(gb),
+                 0 if gb is None else _DT[bdt], B, C, R, stream_of(g))
+        return ga, gb, None
+
+
+def to_tokens(x):
+    """(B, C, L) -> contiguous (B, L, C), same dtype."""
+    return _TransposeAdd.apply(x, None, x.dtype)
+
+
+def to_channels(a, b=None, dtype=None):
+    """(B, L, C) (+ b) -> contiguous (B, C, L)."""
+    return _TransposeAdd.apply(a, b, dtype or a.dtype)
+
+
+def _want_bf16():
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+class _LayerNorm(Function):
+    """y = LayerNorm(a (+ b)) over the last dim -> (y fp32, y bf16 or None)."""
+
+    @staticmethod
+    def forward(ctx, a, b, weight, bias, eps, want16):
+        _cuda_only("layer_norm", a, b)
+        a = a.contiguous()
+        b = None if b is None else b.contiguous()
+        C = a.shape[-1]
+        rows = a.numel() // C
+        y32 = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+        y16 = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device) if want16 else None
+        mean = torch.empty(rows, dtype=torch.float32, device=a.device)
+        rstd = torch.empty_like(mean)
+        w, bb = weight.float().contiguous(), bias.float().contiguous()
+        with torch.cuda.device(a.device):
+            call("layernorm_fwd", lib().pcops_layernorm_fwd, ptr(a), _dt(a), ptr(b), 0 if b is None else _dt(b),
+                 ptr(w), ptr(bb), float(eps), rows, C, ptr(y32), ptr(y16), ptr(mean), ptr(rstd), stream_of(a))
+        ctx.save_for_backward(a, b, w, mean, rstd)
+        ctx.wdt = weight.dtype
+        if y16 is None:
+            return y32
+        return y32, y16
+
+    @staticmethod
+    def backward(ctx, g32, g16=None):
+        a, b, w, mean, rstd = ctx.saved_tensors
+        C = a.shape[-1]
+        rows = a.numel() // C
+        g32 = None if g32 is None else g32.contiguous().float()
+        g16 = None if g16 is None else g16.contiguous().to(torch.bfloat16)
+        dtypes = {a.dtype} | ({b.dtype} if b is not None else set())
+        dx32 = torch.empty(a.shape, dtype=torch.float32, device=a.device) if torch.float32 in dtypes else None
+        dx16 = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device) if torch.bfloat16 in dtypes else None
+        dw = torch.empty(C, dtype=torch.float32, device=a.device)
+        db = torch.empty_like(dw)
+        wsb = lib().pcops_layernorm_bwd_workspace_bytes(rows, C)
+        ws = _lib.Workspace.get(a.device, wsb)
+        with torch.cuda.device(a.device):
+            call("layernorm_bwd", lib().pcops_layernorm_bwd, ptr(g32), ptr(g16), ptr(a), _dt(a), ptr(b),
+                 0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16), ptr(dw),
+                 ptr(db), ptr(ws), wsb, stream_of(a))
+        pick = {torch.float32: dx32, torch.bfloat16: dx16}
+        ga = pick[a.dtype]
+        gb = None if b is None else pick[b.dtype]
+        return ga, gb, dw.to(ctx.wdt), db.to(ctx.wdt), None, None
+
+
+def layer_norm(norm, a, b=None):
+    """norm(a (+ b)) -> (fp32 output, GEMM operand: its bf16 copy under autocast)."""
+    if _want_bf16():
+        return _LayerNorm.apply(a, b, norm.weight, norm.bias, norm.eps, True)
+    y = _LayerNorm.apply(a, b, norm.weight, norm.bias, norm.eps, False)
+    return y, y
+
+
+def _conv1x1_tokens(conv, x_tok):
+    """Conv1d(k=1) applied to token-major (B, L, C_in) input as a GEMM."""
+    return F.linear(x_tok, conv.weight.view(conv.weight.shape[0], -1), conv.bias)
+
+
+class _BlockBase(nn.Module):
+    """Shared body of self_attention / cross_attention / self_attention_woinp."""
+
+    def __init__(self, d_model, d_model_out, nhead, dim_feedforward, dropout, input_proj=True):
+        super().__init__()
+        self.multihead_attn = MultiheadAttention(d_model_out, nhead, dropout=dropout, batch_first=True)
+        self.linear11 = nn.Linear(d_model_out, dim_feedforward)
+        self.dropout1 = nn.Dropout(dropout)
+        self.linear12 = nn.Linear(dim_feedforward, d_model_out)
+        self.norm12 = nn.LayerNorm(d_model_out)
+        self.norm13 = nn.LayerNorm(d_model_out)
+        self.dropout12 = nn.Dropout(dropout)
+        self.dropout13 = nn.Dropout(dropout)
+        self.activation1 = torch.nn.GELU()
+        if input_proj:
+            self.input_proj = nn.Conv1d(d_model, d_model_out, kernel_size=1)
+        if dropout != 0.0:
+            raise NotImplementedError("dropout is 0 in every reference configuration")
+
+    @staticmethod
+    def with_pos_embed(tensor, pos):
+        return tensor if pos is None else tensor + pos
+
+    def _tail(self, s1, attn):
+        """norm12(s1 + attn) -> FFN -> (residual stream fp32, FFN output)."""
+        s2, s2h = layer_norm(self.norm12, s1, attn)
+        f = self.linear12(self.activation1(self.linear11(s2h)))
+        return s2, f
+
+    def _in(self, x_tok):
+        y = _conv1x1_tokens(self.input_proj, x_tok) if hasattr(self, "input_proj") else x_tok
+        return layer_norm(self.norm13, y)
+
+
+def _pos_tokens(pos):
+    # the reference passes pos seq-first (L, B, C)
+    return None if pos is None else pos.transpose(0, 1)
+
+
+class self_attention(_BlockBase):
     """models/model_utils.py:584-617."""
 
     def __init__(self, d_model=256, d_model_out=256, nhead=4, dim_feedforward=1024, dropout=0.0):
-        super().__init__()
-        self.multihead_attn = MultiheadAttention(d_model_out, nhead, dropout=dropout)
-        self.linear11 = nn.Linear(d_model_out, dim_feedforward)
-        self.dropout1 = nn.Dropout(dropout)
-        self.linear12 = nn.Linear(dim_feedforward, d_model_out)
-        self.norm12 = nn.LayerNorm(d_model_out)
-        self.norm13 = nn.LayerNorm(d_model_out)
-        self.dropout12 = nn.Dropout(dropout)
-        self.dropout13 = nn.Dropout(dropout)
-        self.activation1 = torch.nn.GELU()
-        self.input_proj = nn.Conv1d(d_model, d_model_out, kernel_size=1)
+        super().__init__(d_model, d_model_out, nhead, dim_feedforward, dropout)
 
-    def with_pos_embed(self, tensor, pos):
-        return tensor if pos is None else tensor + pos
+    def forward_tokens(self, x_tok, pos=None):
+        """(B, L, C_in) -> (s2, f) with the block output = s2 + f (B, L, C_out)."""
+        s1, s1h = self._in(x_tok)
+        if pos is None:
+            attn = self.multihead_attn(s1h, s1h, s1h)[0]
+        else:
+            q = s1 + pos
+            attn = self.multihead_attn(q, q, s1h)[0]
+        return self._tail(s1, attn)
 
     def forward(self, src1, pos=None):
-        src1 = self.input_proj(src1)
-        b, c, _ = src1.shape
-        src1 = src1.reshape(b, c, -1).permute(2, 0, 1)
-        src1 = self.norm13(src1)
-        q = k = self.with_pos_embed(src1, pos)
-        src12 = self.multihead_attn(query=q, key=k, value=src1)[0]
-        src1 = src1 + self.dropout12(src12)
-        src1 = self.norm12(src1)
-        src12 = self.linear12(self.dropout1(self.activation1(self.linear11(src1))))
-        src1 = src1 + self.dropout13(src12)
-        return src1.permute(1, 2, 0)
+        s2, f = self.forward_tokens(to_tokens(src1), _pos_tokens(pos))
+        return to_channels(s2, f, s2.dtype)
 
 
-class cross_attention(nn.Module):
+class cross_attention(_BlockBase):
     """models/model_utils.py:542-582 (PointSea copy :385-426 is identical)."""
 
     def __init__(self, d_model=256, d_model_out=256, nhead=4, dim_feedforward=1024, dropout=0.0):
-        super().__init__()
-        self.multihead_attn = MultiheadAttention(d_model_out, nhead, dropout=dropout)
-        self.linear11 = nn.Linear(d_model_out, dim_feedforward)
-        self.dropout1 = nn.Dropout(dropout)
-        self.linear12 = nn.Linear(dim_feedforward, d_model_out)
-        self.norm12 = nn.LayerNorm(d_model_out)
-        self.norm13 = nn.LayerNorm(d_model_out)
-        self.dropout12 = nn.Dropout(dropout)
-        self.dropout13 = nn.Dropout(dropout)
-        self.activation1 = torch.nn.GELU()
-        self.input_proj = nn.Conv1d(d_model, d_model_out, kernel_size=1)
+        super().__init__(d_model, d_model_out, nhead, dim_feedforward, dropout)
 
-    def with_pos_embed(self, tensor, pos):
-        return tensor if pos is None else tensor + pos
+    def forward_tokens(self, x1_tok, x2_tok, pos=None):
+        s1, _ = self._in(x1_tok)
+        _, s2h = self._in(x2_tok)
+        q = self.with_pos_embed(s1, pos)
+        attn = self.multihead_attn(q, s2h, s2h)[0]
+        return self._tail(s1, attn)
 
     def forward(self, src1, src2, pos=None):
-        src1 = self.input_proj(src1)
-        src2 = self.input_proj(src2)
-        b, c, _ = src1.shape
-        src1 = src1.reshape(b, c, -1).permute(2, 0, 1)
-        src2 = src2.reshape(b, c, -1).permute(2, 0, 1)
-        src1 = self.norm13(src1)
-        src2 = self.norm13(src2)
-        q = self.with_pos_embed(src1, pos)
-        src12 = self.multihead_attn(query=q, key=src2, value=src2)[0]
-        src1 = src1 + self.dropout12(src12)
-        src1 = self.norm12(src1)
-        src12 = self.linear12(self.dropout1(self.activation1(self.linear11(src1))))
-        src1 = src1 + self.dropout13(src12)
-        return src1.permute(1, 2, 0)
+        s2, f = self.forward_tokens(to_tokens(src1), to_tokens(src2), _pos_tokens(pos))
+        return to_channels(s2, f, s2.dtype)
 
 
-class self_attention_woinp(nn.Module):
+class self_attention_woinp(_BlockBase):
     """models_PointSea/model_utils.py:463-494 (no input projection)."""
 
     def __init__(self, d_model=256, d_model_out=256, nhead=4, dim_feedforward=1024, dropout=0.0):
-        super().__init__()
-        self.multihead_attn = MultiheadAttention(d_model_out, nhead, dropout=dropout)
-        self.linear11 = nn.Linear(d_model_out, dim_feedforward)
-        self.dropout1 = nn.Dropout(dropout)
-        self.linear12 = nn.Linear(dim_feedforward, d_model_out)
-        self.norm12 = nn.LayerNorm(d_model_out)
-        self.norm13 = nn.LayerNorm(d_model_out)
-        self.dropout12 = nn.Dropout(dropout)
-        self.dropout13 = nn.Dropout(dropout)
-        self.activation1 = torch.nn.GELU()
+        super().__init__(d_model, d_model_out, nhead, dim_feedforward, dropout, input_proj=False)
 
-    def with_pos_embed(self, tensor, pos):
-        return tensor if pos is None else tensor + pos
-
-    def forward(self, src1, pos=None):
-        b, c, _ = src1.shape
-        src1 = src1.reshape(b, c, -1).permute(2, 0, 1)
-        src1 = self.norm13(src1)
-        q = k = self.with_pos_embed(src1, pos)
-        src12 = self.multihead_attn(query=q, key=k, value=src1)[0]
-        src1 = src1 + self.dropout12(src12)
-        src1 = self.norm12(src1)
-        src12 = self.linear12(self.dropout1(self.activation1(self.linear11(src1))))
-        src1 = src1 + self.dropout13(src12)
-        return src1.permute(1, 2, 0)
+    forward_tokens = self_attention.forward_tokens
+    forward = self_attention.forward
 
 
 class SDG_Decoder(nn.Module):
-    """models/model_utils.py:619-629."""
+    """models/model_utils.py:619-629; the two blocks hand over token-major."""
 
     def __init__(self, hidden_dim, channel, ratio):
         super().__init__()
         self.sa1 = self_attention(hidden_dim, hidden_dim, dropout=0.0, nhead=8)
         self.sa2 = self_attention(hidden_dim, channel * ratio, dropout=0.0, nhead=8)
 
+    def forward_tokens(self, x_tok):
+        s, f = self.sa1.forward_tokens(x_tok)
+        s, f = self.sa2.forward_tokens(s + f)
+        return s + f
+
     def forward(self, input):
-        return self.sa2(self.sa1(input))
+        s, f = self.sa1.forward_tokens(to_tokens(input))
+        s, f = self.sa2.forward_tokens(s + f)
+        return to_channels(s, f, s.dtype)
 
 
 class SDG_Decoder_PointSea(nn.Module):
@@ -251,4 +419,6 @@ class SDG_Decoder_PointSea(nn.Module):
         self.sa2 = self_attention_woinp(hidden_dim, hidden_dim, dropout=dropout, nhead=8)
 
     def forward(self, input, pos=None):
-        return self.sa2(self.sa1(input))
+        s, f = self.sa1.forward_tokens(to_tokens(input))
+        s, f = self.sa2.forward_tokens(s + f)
+        return to_channels(s, f, s.dtype)

@@ -180,8 +180,16 @@ __device__ __forceinline__ void store_Y(const f32x16 (&Y)[D / 32], T *base, long
     }
 }
 
+// Element (b, h, row, d) of a tensor lives at b*sb + h*sh + row*srow + d, so
+// seq-first (L, B, H*hd) [sb = H*hd, sh = hd, srow = B*H*hd] and batch-first
+// (B, L, H*hd) [sb = L*H*hd, sh = hd, srow = H*hd] layouts are both read in place.
 struct Strides {
-  long long q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow;
+  long long q_sb, q_sh, q_srow, k_sb, k_sh, k_srow, v_sb, v_sh, v_srow, o_sb, o_sh, o_srow;
+  int H;
+  __device__ __forceinline__ long long q_off(int bh) const { return (long long)(bh / H) * q_sb + (long long)(bh % H) * q_sh; }
+  __device__ __forceinline__ long long k_off(int bh) const { return (long long)(bh / H) * k_sb + (long long)(bh % H) * k_sh; }
+  __device__ __forceinline__ long long v_off(int bh) const { return (long long)(bh / H) * v_sb + (long long)(bh % H) * v_sh; }
+  __device__ __forceinline__ long long o_off(int bh) const { return (long long)(bh / H) * o_sb + (long long)(bh % H) * o_sh; }
 };
 
 // ----------------------------------------------------------------- forward
@@ -198,9 +206,9 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const T *__restrict_
   const int q0 = blockIdx.x * (kWaves * 32) + w * 32;
   const int qi = q0 + (l & 31);
   typename P::Frag qf;
-  P::load_frag(qf, Q + bh * st.q_sbh + (long long)(qi < Lq ? qi : 0) * st.q_srow, qi < Lq);
-  const T *Kb = K + bh * st.k_sbh;
-  const T *Vb = V + bh * st.v_sbh;
+  P::load_frag(qf, Q + st.q_off(bh) + (long long)(qi < Lq ? qi : 0) * st.q_srow, qi < Lq);
+  const T *Kb = K + st.k_off(bh);
+  const T *Vb = V + st.v_off(bh);
   const float sl2 = scale * kLog2e;
   float m = -INFINITY, lsum = 0.f;
   f32x16 Y[D / 32];
@@ -240,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const T *__restrict_
     P::product2(Y, sv, X);
     __syncthreads();
   }
-  store_Y<T, D>(Y, O + bh * st.o_sbh, st.o_srow, q0, Lq, 1.f / lsum);
+  store_Y<T, D>(Y, O + st.o_off(bh), st.o_srow, q0, Lq, 1.f / lsum);
   if (h == 0 && qi < Lq && lse) lse[(long long)bh * Lq + qi] = (m + log2f(lsum)) * kLn2;
 }
 
@@ -251,8 +259,8 @@ __global__ void attn_delta_kernel(const T *__restrict__ O, const T *__restrict__
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= BH * Lq) return;
   const int bh = row / Lq, q = row - bh * Lq;
-  const T *o = O + bh * st.o_sbh + (long long)q * st.o_srow;
-  const T *g = dO + bh * st.o_sbh + (long long)q * st.o_srow;
+  const T *o = O + st.o_off(bh) + (long long)q * st.o_srow;
+  const T *g = dO + st.o_off(bh) + (long long)q * st.o_srow;
   float s = 0.f;
   for (int d = lane_(); d < D; d += 64) s += Prec<T, 32>::to_f(o[d]) * Prec<T, 32>::to_f(g[d]);
   s = wave_sum_f32(s);
@@ -275,12 +283,12 @@ __global__ __launch_bounds__(kThreads) void attn_dq_kernel(const T *__restrict__
   const int qi = q0 + (l & 31);
   const bool qv = qi < Lq;
   typename P::Frag qf, gf;
-  P::load_frag(qf, Q + bh * st.q_sbh + (long long)(qv ? qi : 0) * st.q_srow, qv);
-  P::load_frag(gf, dO + bh * st.o_sbh + (long long)(qv ? qi : 0) * st.o_srow, qv);
+  P::load_frag(qf, Q + st.q_off(bh) + (long long)(qv ? qi : 0) * st.q_srow, qv);
+  P::load_frag(gf, dO + st.o_off(bh) + (long long)(qv ? qi : 0) * st.o_srow, qv);
   const float lse2 = qv ? lse[(long long)bh * Lq + qi] * kLog2e : INFINITY;
   const float dl = qv ? delta[(long long)bh * Lq + qi] : 0.f;
-  const T *Kb = K + bh * st.k_sbh;
-  const T *Vb = V + bh * st.v_sbh;
+  const T *Kb = K + st.k_off(bh);
+  const T *Vb = V + st.v_off(bh);
   const float sl2 = scale * kLog2e;
   f32x16 Y[D / 32];
 #pragma unroll
@@ -300,7 +308,7 @@ __global__ __launch_bounds__(kThreads) void attn_dq_kernel(const T *__restrict__
     P::product2(Y, sk, S);
     __syncthreads();
   }
-  store_Y<T, D>(Y, dQ + bh * st.q_sbh, st.q_srow, q0, Lq, scale);
+  store_Y<T, D>(Y, dQ + st.q_off(bh), st.q_srow, q0, Lq, scale);
 }
 
 // ----------------------------------------------------------------- dK/dV pass
@@ -321,10 +329,10 @@ __global__ __launch_bounds__(kThreads) void attn_dkv_kernel(const T *__restrict_
   const int ki = k0w + (l & 31);
   const bool kv = ki < Lk;
   typename P::Frag kf, vf;
-  P::load_frag(kf, K + bh * st.k_sbh + (long long)(kv ? ki : 0) * st.k_srow, kv);
-  P::load_frag(vf, V + bh * st.v_sbh + (long long)(kv ? ki : 0) * st.v_srow, kv);
-  const T *Qb = Q + bh * st.q_sbh;
-  const T *Gb = dO + bh * st.o_sbh;
+  P::load_frag(kf, K + st.k_off(bh) + (long long)(kv ? ki : 0) * st.k_srow, kv);
+  P::load_frag(vf, V + st.v_off(bh) + (long long)(kv ? ki : 0) * st.v_srow, kv);
+  const T *Qb = Q + st.q_off(bh);
+  const T *Gb = dO + st.o_off(bh);
   const float sl2 = scale * kLog2e;
   f32x16 Y1[D / 32], Y2[D / 32];
 #pragma unroll
@@ -355,8 +363,8 @@ __global__ __launch_bounds__(kThreads) void attn_dkv_kernel(const T *__restrict_
     P::product2(Y2, sq, G);  // dK^T += Q^T dS
     __syncthreads();
   }
-  store_Y<T, D>(Y1, dV + bh * st.v_sbh, st.v_srow, k0w, Lk, 1.f);
-  store_Y<T, D>(Y2, dK + bh * st.k_sbh, st.k_srow, k0w, Lk, scale);
+  store_Y<T, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
+  store_Y<T, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
 }
 
 // ----------------------------------------------------------------- forward, bf16 (v2)
@@ -468,12 +476,12 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
   const int qi = q0 + (l & 31);
   bf16x8 qf[D / 16];
   {
-    const __bf16 *row = Q + bh * st.q_sbh + (long long)(qi < Lq ? qi : 0) * st.q_srow + 8 * h;
+    const __bf16 *row = Q + st.q_off(bh) + (long long)(qi < Lq ? qi : 0) * st.q_srow + 8 * h;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) qf[s] = qi < Lq ? *reinterpret_cast<const bf16x8 *>(row + 16 * s) : bf16x8{};
   }
-  const __bf16 *Kb = K + bh * st.k_sbh;
-  const __bf16 *Vb = V + bh * st.v_sbh;
+  const __bf16 *Kb = K + st.k_off(bh);
+  const __bf16 *Vb = V + st.v_off(bh);
   const float sl2 = scale * kLog2e;
   float m = -INFINITY, lsum = 0.f;
   f32x16 Y[D / 32];
@@ -525,7 +533,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   }
-  store_Y<__bf16, D>(Y, O + bh * st.o_sbh, st.o_srow, q0, Lq, 1.f / lsum);
+  store_Y<__bf16, D>(Y, O + st.o_off(bh), st.o_srow, q0, Lq, 1.f / lsum);
   if (h == 0 && qi < Lq && lse) lse[(long long)bh * Lq + qi] = (m + log2f(lsum)) * kLn2;
 }
 
@@ -562,8 +570,8 @@ __global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restr
   const bool qv = qi < Lq;
   bf16x8 qf[D / 16], gf[D / 16];
   {
-    const __bf16 *qr = Q + bh * st.q_sbh + (long long)(qv ? qi : 0) * st.q_srow + 8 * h;
-    const __bf16 *gr = dO + bh * st.o_sbh + (long long)(qv ? qi : 0) * st.o_srow + 8 * h;
+    const __bf16 *qr = Q + st.q_off(bh) + (long long)(qv ? qi : 0) * st.q_srow + 8 * h;
+    const __bf16 *gr = dO + st.o_off(bh) + (long long)(qv ? qi : 0) * st.o_srow + 8 * h;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       qf[s] = qv ? *reinterpret_cast<const bf16x8 *>(qr + 16 * s) : bf16x8{};
@@ -572,8 +580,8 @@ __global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restr
   }
   const float lse2 = qv ? lse[(long long)bh * Lq + qi] * kLog2e : INFINITY;
   const float dl = qv ? delta[(long long)bh * Lq + qi] : 0.f;
-  const __bf16 *Kb = K + bh * st.k_sbh;
-  const __bf16 *Vb = V + bh * st.v_sbh;
+  const __bf16 *Kb = K + st.k_off(bh);
+  const __bf16 *Vb = V + st.v_off(bh);
   const float sl2 = scale * kLog2e;
   f32x16 Y[D / 32];
 #pragma unroll
@@ -611,7 +619,7 @@ __global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restr
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   }
-  store_Y<__bf16, D>(Y, dQ + bh * st.q_sbh, st.q_srow, q0, Lq, scale);
+  store_Y<__bf16, D>(Y, dQ + st.q_off(bh), st.q_srow, q0, Lq, scale);
 }
 
 // dK/dV pass: keys on the lane, Q/dO 64-row tiles (+ their lse/delta) double-buffered.
@@ -637,16 +645,16 @@ __global__ __launch_bounds__(NW * 64) void attn_dkv2_kernel(const __bf16 *__rest
   const bool kv = ki < Lk;
   bf16x8 kf[D / 16], vf[D / 16];
   {
-    const __bf16 *kr0 = K + bh * st.k_sbh + (long long)(kv ? ki : 0) * st.k_srow + 8 * h;
-    const __bf16 *vr0 = V + bh * st.v_sbh + (long long)(kv ? ki : 0) * st.v_srow + 8 * h;
+    const __bf16 *kr0 = K + st.k_off(bh) + (long long)(kv ? ki : 0) * st.k_srow + 8 * h;
+    const __bf16 *vr0 = V + st.v_off(bh) + (long long)(kv ? ki : 0) * st.v_srow + 8 * h;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       kf[s] = kv ? *reinterpret_cast<const bf16x8 *>(kr0 + 16 * s) : bf16x8{};
       vf[s] = kv ? *reinterpret_cast<const bf16x8 *>(vr0 + 16 * s) : bf16x8{};
     }
   }
-  const __bf16 *Qb = Q + bh * st.q_sbh;
-  const __bf16 *Gb = dO + bh * st.o_sbh;
+  const __bf16 *Qb = Q + st.q_off(bh);
+  const __bf16 *Gb = dO + st.o_off(bh);
   const float *lse_b = lse + (long long)bh * Lq;
   const float *dl_b = delta + (long long)bh * Lq;
   const float sl2 = scale * kLog2e;
@@ -713,8 +721,8 @@ __global__ __launch_bounds__(NW * 64) void attn_dkv2_kernel(const __bf16 *__rest
     }
     lds_barrier();
   }
-  store_Y<__bf16, D>(Y1, dV + bh * st.v_sbh, st.v_srow, k0w, Lk, 1.f);
-  store_Y<__bf16, D>(Y2, dK + bh * st.k_sbh, st.k_srow, k0w, Lk, scale);
+  store_Y<__bf16, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
+  store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
 }
 
 template <int D, int NW>
@@ -815,9 +823,9 @@ bool use_v1() {
   return v != 0;
 }
 
-bool aligned_ok(const void *p, long long s_bh, long long s_row, int esize) {
+bool aligned_ok(const void *p, long long sb, long long sh, long long srow, int esize) {
   const int vec = 16 / esize;
-  return ((uintptr_t)p % 16 == 0) && (s_bh % vec == 0) && (s_row % vec == 0);
+  return ((uintptr_t)p % 16 == 0) && (sb % vec == 0) && (sh % vec == 0) && (srow % vec == 0);
 }
 
 template <typename T>
@@ -904,62 +912,70 @@ int check_common(int BH, int Lq, int Lk, int D, int dtype) {
 
 }  // namespace
 
-extern "C" int pcops_attention_forward(const void *q, const void *k, const void *v, void *o, float *lse, int BH,
-                                       int Lq, int Lk, int D, float scale, int dtype, long long q_sbh,
-                                       long long q_srow, long long k_sbh, long long k_srow, long long v_sbh,
-                                       long long v_srow, long long o_sbh, long long o_srow, pcops_stream_t stream) {
-  if (BH < 0 || Lq < 0 || Lk < 0) return PCOPS_ERR_INVALID;
+#define PC_ATTN_STRIDES                                                                                     \
+  long long q_sb, long long q_sh, long long q_srow, long long k_sb, long long k_sh, long long k_srow, long long v_sb, \
+      long long v_sh, long long v_srow, long long o_sb, long long o_sh, long long o_srow
+#define PC_ATTN_STRIDE_ARGS q_sb, q_sh, q_srow, k_sb, k_sh, k_srow, v_sb, v_sh, v_srow, o_sb, o_sh, o_srow
+
+extern "C" int pcops_attention_forward(const void *q, const void *k, const void *v, void *o, float *lse, int B, int H,
+                                       int Lq, int Lk, int D, float scale, int dtype, PC_ATTN_STRIDES,
+                                       pcops_stream_t stream) {
+  if (B < 0 || H <= 0 || Lq < 0 || Lk < 0) return PCOPS_ERR_INVALID;
+  const int BH = B * H;
   if (BH == 0 || Lq == 0) return PCOPS_OK;
   if (Lk <= 0 || !q || !k || !v || !o) return PCOPS_ERR_INVALID;
   if (D % 32 != 0 || D > 128 || (dtype != 0 && dtype != 1)) return PCOPS_ERR_UNSUPPORTED;
   const int es = dtype == 0 ? 4 : 2;
-  if (!aligned_ok(q, q_sbh, q_srow, es) || !aligned_ok(k, k_sbh, k_srow, es) || !aligned_ok(v, v_sbh, v_srow, es) ||
-      !aligned_ok(o, o_sbh, o_srow, es))
+  if (!aligned_ok(q, q_sb, q_sh, q_srow, es) || !aligned_ok(k, k_sb, k_sh, k_srow, es) ||
+      !aligned_ok(v, v_sb, v_sh, v_srow, es) || !aligned_ok(o, o_sb, o_sh, o_srow, es))
     return PCOPS_ERR_UNSUPPORTED;
-  const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
+  const Strides st{PC_ATTN_STRIDE_ARGS, H};
   hipStream_t s = (hipStream_t)stream;
   if (dtype == 0) return launch_fwd<float>(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s);
   if (use_v1()) return launch_fwd<__bf16>(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s);
   return fwd2_dispatch(q, k, v, o, lse, BH, Lq, Lk, D, scale, st, s);
 }
 
-extern "C" unsigned long long pcops_attention_bwd_workspace_bytes(int BH, int Lq, int Lk, int D) {
+extern "C" unsigned long long pcops_attention_bwd_workspace_bytes(int B, int H, int Lq, int Lk, int D) {
   (void)Lk;
   (void)D;
-  if (BH <= 0 || Lq <= 0) return 0;
-  return (unsigned long long)BH * Lq * sizeof(float);
+  if (B <= 0 || H <= 0 || Lq <= 0) return 0;
+  return (unsigned long long)B * H * Lq * sizeof(float);
 }
 
-extern "C" int pcops_attention_bwd_preprocess(const void *o, const void *dout, int BH, int Lq, int D, int dtype,
-                                              long long o_sbh, long long o_srow, void *workspace,
+extern "C" int pcops_attention_bwd_preprocess(const void *o, const void *dout, int B, int H, int Lq, int D, int dtype,
+                                              long long o_sb, long long o_sh, long long o_srow, void *workspace,
                                               unsigned long long workspace_bytes, pcops_stream_t stream) {
-  int rc = check_common(BH, Lq, 1, D, dtype);
+  if (B < 0 || H <= 0 || Lq < 0) return PCOPS_ERR_INVALID;
+  int rc = check_common(B * H, Lq, 1, D, dtype);
   if (rc) return rc;
+  const int BH = B * H;
   if (BH == 0 || Lq == 0) return PCOPS_OK;
   if (!o || !dout) return PCOPS_ERR_INVALID;
-  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(BH, Lq, 1, D)) return PCOPS_ERR_WORKSPACE;
-  const Strides st{0, 0, 0, 0, 0, 0, o_sbh, o_srow};
+  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(B, H, Lq, 1, D)) return PCOPS_ERR_WORKSPACE;
+  const Strides st{0, 0, 0, 0, 0, 0, 0, 0, 0, o_sb, o_sh, o_srow, H};
   hipStream_t s = (hipStream_t)stream;
   return dtype == 0 ? launch_delta<float>(o, dout, (float *)workspace, BH, Lq, D, st, s)
                     : launch_delta<__bf16>(o, dout, (float *)workspace, BH, Lq, D, st, s);
 }
 
 extern "C" int pcops_attention_bwd_dq(const void *q, const void *k, const void *v, const void *dout, const float *lse,
-                                      void *dq, int BH, int Lq, int Lk, int D, float scale, int dtype,
-                                      long long q_sbh, long long q_srow, long long k_sbh, long long k_srow,
-                                      long long v_sbh, long long v_srow, long long o_sbh, long long o_srow,
-                                      const void *workspace, unsigned long long workspace_bytes,
+                                      void *dq, int B, int H, int Lq, int Lk, int D, float scale, int dtype,
+                                      PC_ATTN_STRIDES, const void *workspace, unsigned long long workspace_bytes,
                                       pcops_stream_t stream) {
-  int rc = check_common(BH, Lq, Lk, D, dtype);
+  if (B < 0 || H <= 0) return PCOPS_ERR_INVALID;
+  int rc = check_common(B * H, Lq, Lk, D, dtype);
   if (rc) return rc;
+  const int BH = B * H;
   if (BH == 0 || Lq == 0) return PCOPS_OK;
   if (!q || !k || !v || !dout || !lse || !dq || Lk <= 0) return PCOPS_ERR_INVALID;
-  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(BH, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(B, H, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
   const int es = dtype == 0 ? 4 : 2;
-  if (!aligned_ok(q, q_sbh, q_srow, es) || !aligned_ok(k, k_sbh, k_srow, es) || !aligned_ok(v, v_sbh, v_srow, es) ||
-      !aligned_ok(dout, o_sbh, o_srow, es) || !aligned_ok(dq, q_sbh, q_srow, es))
+  if (!aligned_ok(q, q_sb, q_sh, q_srow, es) || !aligned_ok(k, k_sb, k_sh, k_srow, es) ||
+      !aligned_ok(v, v_sb, v_sh, v_srow, es) || !aligned_ok(dout, o_sb, o_sh, o_srow, es) ||
+      !aligned_ok(dq, q_sb, q_sh, q_srow, es))
     return PCOPS_ERR_UNSUPPORTED;
-  const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
+  const Strides st{PC_ATTN_STRIDE_ARGS, H};
   hipStream_t s = (hipStream_t)stream;
   const float *delta = (const float *)workspace;
   if (dtype == 0) return launch_dq<float>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s);
@@ -968,21 +984,22 @@ extern "C" int pcops_attention_bwd_dq(const void *q, const void *k, const void *
 }
 
 extern "C" int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const void *dout,
-                                       const float *lse, void *dk, void *dv, int BH, int Lq, int Lk, int D,
-                                       float scale, int dtype, long long q_sbh, long long q_srow, long long k_sbh,
-                                       long long k_srow, long long v_sbh, long long v_srow, long long o_sbh,
-                                       long long o_srow, const void *workspace, unsigned long long workspace_bytes,
-                                       pcops_stream_t stream) {
-  int rc = check_common(BH, Lq, Lk, D, dtype);
+                                       const float *lse, void *dk, void *dv, int B, int H, int Lq, int Lk, int D,
+                                       float scale, int dtype, PC_ATTN_STRIDES, const void *workspace,
+                                       unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (B < 0 || H <= 0) return PCOPS_ERR_INVALID;
+  int rc = check_common(B * H, Lq, Lk, D, dtype);
   if (rc) return rc;
+  const int BH = B * H;
   if (BH == 0 || Lk == 0) return PCOPS_OK;
   if (!q || !k || !v || !dout || !lse || !dk || !dv || Lq <= 0) return PCOPS_ERR_INVALID;
-  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(BH, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(B, H, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
   const int es = dtype == 0 ? 4 : 2;
-  if (!aligned_ok(q, q_sbh, q_srow, es) || !aligned_ok(k, k_sbh, k_srow, es) || !aligned_ok(v, v_sbh, v_srow, es) ||
-      !aligned_ok(dout, o_sbh, o_srow, es) || !aligned_ok(dk, k_sbh, k_srow, es) || !aligned_ok(dv, v_sbh, v_srow, es))
+  if (!aligned_ok(q, q_sb, q_sh, q_srow, es) || !aligned_ok(k, k_sb, k_sh, k_srow, es) ||
+      !aligned_ok(v, v_sb, v_sh, v_srow, es) || !aligned_ok(dout, o_sb, o_sh, o_srow, es) ||
+      !aligned_ok(dk, k_sb, k_sh, k_srow, es) || !aligned_ok(dv, v_sb, v_sh, v_srow, es))
     return PCOPS_ERR_UNSUPPORTED;
-  const Strides st{q_sbh, q_srow, k_sbh, k_srow, v_sbh, v_srow, o_sbh, o_srow};
+  const Strides st{PC_ATTN_STRIDE_ARGS, H};
   hipStream_t s = (hipStream_t)stream;
   const float *delta = (const float *)workspace;
   if (dtype == 0) return launch_dkv<float>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
@@ -992,19 +1009,19 @@ extern "C" int pcops_attention_bwd_dkv(const void *q, const void *k, const void 
 
 // dq/dk/dv use the q/k/v strides; dout uses the o strides.
 extern "C" int pcops_attention_backward(const void *q, const void *k, const void *v, const void *o, const void *dout,
-                                        const float *lse, void *dq, void *dk, void *dv, int BH, int Lq, int Lk, int D,
-                                        float scale, int dtype, long long q_sbh, long long q_srow, long long k_sbh,
-                                        long long k_srow, long long v_sbh, long long v_srow, long long o_sbh,
-                                        long long o_srow, void *workspace, unsigned long long workspace_bytes,
-                                        pcops_stream_t stream) {
-  if (BH == 0 || Lq == 0 || Lk == 0) return check_common(BH, Lq, Lk, D, dtype);
+                                        const float *lse, void *dq, void *dk, void *dv, int B, int H, int Lq, int Lk,
+                                        int D, float scale, int dtype, PC_ATTN_STRIDES, void *workspace,
+                                        unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (B < 0 || H <= 0) return PCOPS_ERR_INVALID;
+  if (B == 0 || Lq == 0 || Lk == 0) return check_common(B * H, Lq, Lk, D, dtype);
   const int es = dtype == 0 ? 4 : 2;
-  if (o && !aligned_ok(o, o_sbh, o_srow, es)) return PCOPS_ERR_UNSUPPORTED;
-  int rc = pcops_attention_bwd_preprocess(o, dout, BH, Lq, D, dtype, o_sbh, o_srow, workspace, workspace_bytes, stream);
+  if (o && !aligned_ok(o, o_sb, o_sh, o_srow, es)) return PCOPS_ERR_UNSUPPORTED;
+  int rc = pcops_attention_bwd_preprocess(o, dout, B, H, Lq, D, dtype, o_sb, o_sh, o_srow, workspace, workspace_bytes,
+                                          stream);
   if (rc) return rc;
-  rc = pcops_attention_bwd_dq(q, k, v, dout, lse, dq, BH, Lq, Lk, D, scale, dtype, q_sbh, q_srow, k_sbh, k_srow, v_sbh,
-                              v_srow, o_sbh, o_srow, workspace, workspace_bytes, stream);
+  rc = pcops_attention_bwd_dq(q, k, v, dout, lse, dq, B, H, Lq, Lk, D, scale, dtype, PC_ATTN_STRIDE_ARGS, workspace,
+                              workspace_bytes, stream);
   if (rc) return rc;
-  return pcops_attention_bwd_dkv(q, k, v, dout, lse, dk, dv, BH, Lq, Lk, D, scale, dtype, q_sbh, q_srow, k_sbh, k_srow,
-                                 v_sbh, v_srow, o_sbh, o_srow, workspace, workspace_bytes, stream);
+  return pcops_attention_bwd_dkv(q, k, v, dout, lse, dk, dv, B, H, Lq, Lk, D, scale, dtype, PC_ATTN_STRIDE_ARGS,
+                                 workspace, workspace_bytes, stream);
 }

@@ -1,0 +1,320 @@
+// Memory-bound glue of the attention blocks (models/model_utils.py:542-617):
+// the (B, C, L) <-> (B, L, C) layout changes around the blocks and the two
+// LayerNorms (norm13, norm12 after the residual add), fused so every
+// activation is read and written once per pass.
+//
+//   pcops_transpose_add : out[b][c][r] = a[b][r][c] (+ b[b][r][c]), LDS-tiled
+//                         64x64 transpose, optional second output dtype
+//   pcops_layernorm_fwd : y = LN(a (+ b)) * gamma + beta per row, fp32 and/or
+//                         bf16 outputs, per-row mean / rstd saved
+//   pcops_layernorm_bwd : dx = rstd * (g - mean(g) - xhat * mean(g * xhat)),
+//                         g = (dy32 + dy16) * gamma; dgamma / dbeta as per-wave
+//                         partial sums in a scratch, then a column reduction
+// dtype codes: 0 = fp32, 1 = bf16.  One wave per row for the LayerNorms
+// (C <= 1024, C % 8 == 0: 16-B vector loads, two-pass statistics in registers).
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float ld(const void *p, int dt, long long i) {
+  return dt == 0 ? reinterpret_cast<const float *>(p)[i] : (float)reinterpret_cast<const __bf16 *>(p)[i];
+}
+__device__ __forceinline__ void st(void *p, int dt, long long i, float v) {
+  if (dt == 0)
+    reinterpret_cast<float *>(p)[i] = v;
+  else
+    reinterpret_cast<__bf16 *>(p)[i] = (__bf16)v;
+}
+
+// ---------------------------------------------------------------- transpose
+constexpr int kT = 64;
+
+__global__ __launch_bounds__(256) void transpose_add_kernel(const void *__restrict__ a, int adt,
+                                                            const void *__restrict__ b, int bdt, void *__restrict__ out,
+                                                            int odt, void *__restrict__ out2, int o2dt, int R, int C) {
+  __shared__ float tile[kT][kT + 1];
+  const int bb = blockIdx.z;
+  const int r0 = blockIdx.y * kT, c0 = blockIdx.x * kT;
+  const long long in_base = (long long)bb * R * C, out_base = (long long)bb * C * R;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+#pragma unroll 4
+  for (int i = ty; i < kT; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    float v = 0.f;
+    if (r < R && c < C) {
+      const long long e = in_base + (long long)r * C + c;
+      v = ld(a, adt, e);
+      if (b) v += ld(b, bdt, e);
+    }
+    tile[i][tx] = v;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = ty; i < kT; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (r < R && c < C) {
+      const long long e = out_base + (long long)c * R + r;
+      const float v = tile[tx][i];
+      st(out, odt, e, v);
+      if (out2) st(out2, o2dt, e, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// A row is read as 8-element chunks (one 16-B load for bf16, two for fp32);
+// chunk ch = lane + 64*i, so C <= 1024 needs at most 2 chunks per lane.
+constexpr int kMaxCh = 2;
+
+struct V8 {
+  float v[8];
+};
+
+__device__ __forceinline__ void ld8(V8 &o, const void *p, int dt, long long e) {
+  if (dt == 0) {
+    const float4 x = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + e);
+    const float4 y = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + e + 4);
+    o.v[0] = x.x, o.v[1] = x.y, o.v[2] = x.z, o.v[3] = x.w, o.v[4] = y.x, o.v[5] = y.y, o.v[6] = y.z, o.v[7] = y.w;
+  } else {
+    typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+    const bf16x8_t x = *reinterpret_cast<const bf16x8_t *>(reinterpret_cast<const __bf16 *>(p) + e);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = (float)x[k];
+  }
+}
+__device__ __forceinline__ void st8_f32(float *p, long long e, const V8 &o) {
+  *reinterpret_cast<float4 *>(p + e) = make_float4(o.v[0], o.v[1], o.v[2], o.v[3]);
+  *reinterpret_cast<float4 *>(p + e + 4) = make_float4(o.v[4], o.v[5], o.v[6], o.v[7]);
+}
+__device__ __forceinline__ void st8_bf16(__bf16 *p, long long e, const V8 &o) {
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  bf16x8_t x;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = (__bf16)o.v[k];
+  *reinterpret_cast<bf16x8_t *>(p + e) = x;
+}
+
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a, int adt, const void *__restrict__ b,
+                                                     int bdt, const float *__restrict__ gamma,
+                                                     const float *__restrict__ beta, float eps, int rows, int C,
+                                                     float *__restrict__ y32, __bf16 *__restrict__ y16,
+                                                     float *__restrict__ mean_out, float *__restrict__ rstd_out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int nch = C >> 3;
+  const long long base = (long long)row * C;
+  V8 x[kMaxCh];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxCh; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < nch) {
+      ld8(x[i], a, adt, base + 8 * ch);
+      if (b) {
+        V8 t;
+        ld8(t, b, bdt, base + 8 * ch);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[i].v[k] += t.v[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += x[i].v[k];
+    }
+  }
+  const float mean = wave_sum_f32(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxCh; ++i)
+    if (lane + 64 * i < nch)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = x[i].v[k] - mean;
+        q = __builtin_fmaf(d, d, q);
+      }
+  const float rstd = 1.f / sqrtf(wave_sum_f32(q) / (float)C + eps);
+#pragma unroll
+  for (int i = 0; i < kMaxCh; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < nch) {
+      V8 y;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) y.v[k] = (x[i].v[k] - mean) * rstd * gamma[8 * ch + k] + beta[8 * ch + k];
+      if (y32) st8_f32(y32, base + 8 * ch, y);
+      if (y16) st8_bf16(y16, base + 8 * ch, y);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// One wave per row, grid-stride; dgamma / dbeta partial sums per wave go to
+// a [waves][2][C] scratch (plain stores: thousands of waves atomically adding
+// into the same 2*C floats would serialise), reduced by ln_colsum_kernel.
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g32, const __bf16 *__restrict__ g16,
+                                                     const void *__restrict__ a, int adt, const void *__restrict__ b,
+                                                     int bdt, const float *__restrict__ gamma,
+                                                     const float *__restrict__ mean_in,
+                                                     const float *__restrict__ rstd_in, int rows, int C,
+                                                     float *__restrict__ dx32, __bf16 *__restrict__ dx16,
+                                                     float *__restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int nch = C >> 3;
+  V8 dg[kMaxCh], db[kMaxCh];
+#pragma unroll
+  for (int i = 0; i < kMaxCh; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dg[i].v[k] = db[i].v[k] = 0.f;
+  for (int row = wave; row < rows; row += nwaves) {
+    const long long base = (long long)row * C;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    V8 xh[kMaxCh], g[kMaxCh];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxCh; ++i) {
+      const int ch = lane + 64 * i;
+      if (ch < nch) {
+        V8 x, dy, t;
+        ld8(x, a, adt, base + 8 * ch);
+        if (b) {
+          ld8(t, b, bdt, base + 8 * ch);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x.v[k] += t.v[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dy.v[k] = 0.f;
+        if (g32) {
+          ld8(t, g32, 0, base + 8 * ch);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dy.v[k] += t.v[k];
+        }
+        if (g16) {
+          ld8(t, g16, 1, base + 8 * ch);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dy.v[k] += t.v[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[i].v[k] = (x.v[k] - mean) * rstd;
+          dg[i].v[k] = __builtin_fmaf(dy.v[k], xh[i].v[k], dg[i].v[k]);
+          db[i].v[k] += dy.v[k];
+          g[i].v[k] = dy.v[k] * gamma[8 * ch + k];
+          sg += g[i].v[k];
+          sgx = __builtin_fmaf(g[i].v[k], xh[i].v[k], sgx);
+        }
+      }
+    }
+    const float mg = wave_sum_f32(sg) / (float)C;
+    const float mgx = wave_sum_f32(sgx) / (float)C;
+#pragma unroll
+    for (int i = 0; i < kMaxCh; ++i) {
+      const int ch = lane + 64 * i;
+      if (ch < nch) {
+        V8 dx;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dx.v[k] = rstd * (g[i].v[k] - mg - xh[i].v[k] * mgx);
+        if (dx32) st8_f32(dx32, base + 8 * ch, dx);
+        if (dx16) st8_bf16(dx16, base + 8 * ch, dx);
+      }
+    }
+  }
+  float *pw = part + (long long)wave * 2 * C;
+#pragma unroll
+  for (int i = 0; i < kMaxCh; ++i) {
+    const int ch = lane + 64 * i;
+    if (ch < nch) {
+      st8_f32(pw, 8 * ch, dg[i]);
+      st8_f32(pw + C, 8 * ch, db[i]);
+    }
+  }
+}
+
+// out[c] = sum_w part[w][c] for 2*C columns (dgamma then dbeta)
+__global__ __launch_bounds__(256) void ln_colsum_kernel(const float *__restrict__ part, int waves, int C2,
+                                                        float *__restrict__ dgamma, float *__restrict__ dbeta, int C) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r = threadIdx.x >> 6;
+  float s = 0.f;
+  if (col < C2)
+    for (int w = r; w < waves; w += 4) s += part[(long long)w * C2 + col];
+  red[r][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (r == 0 && col < C2) {
+    const float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+    if (col < C)
+      dgamma[col] = t;
+    else
+      dbeta[col - C] = t;
+  }
+}
+
+constexpr int kLnBwdWaves = 1024;
+
+int ln_bwd_waves(int rows) { return ((rows < kLnBwdWaves ? rows : kLnBwdWaves) + 3) / 4 * 4; }
+
+bool dt_ok(int dt) { return dt == 0 || dt == 1; }
+
+}  // namespace
+
+extern "C" int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype,
+                                   void *out2, int out2_dtype, int B, int R, int C, pcops_stream_t stream) {
+  if (B < 0 || R < 0 || C < 0) return PCOPS_ERR_INVALID;
+  if (B == 0 || R == 0 || C == 0) return PCOPS_OK;
+  if (!a || !out || !dt_ok(a_dtype) || !dt_ok(out_dtype) || (b && !dt_ok(b_dtype)) || (out2 && !dt_ok(out2_dtype)))
+    return PCOPS_ERR_INVALID;
+  const dim3 grid((C + kT - 1) / kT, (R + kT - 1) / kT, B);
+  hipLaunchKernelGGL(transpose_add_kernel, grid, dim3(256), 0, (hipStream_t)stream, a, a_dtype, b, b_dtype, out,
+                     out_dtype, out2, out2_dtype, R, C);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_layernorm_fwd(const void *a, int a_dtype, const void *b, int b_dtype, const float *gamma,
+                                   const float *beta, float eps, int rows, int C, float *y32, void *y16, float *mean,
+                                   float *rstd, pcops_stream_t stream) {
+  if (rows < 0 || C <= 0) return PCOPS_ERR_INVALID;
+  if (rows == 0) return PCOPS_OK;
+  if (C > 512 * kMaxCh || C % 8) return PCOPS_ERR_UNSUPPORTED;
+  if (!a || !gamma || !beta || !mean || !rstd || (!y32 && !y16) || !dt_ok(a_dtype) || (b && !dt_ok(b_dtype)))
+    return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, a, a_dtype, b, b_dtype,
+                     gamma, beta, eps, rows, C, y32, (__bf16 *)y16, mean, rstd);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" unsigned long long pcops_layernorm_bwd_workspace_bytes(int rows, int C) {
+  if (rows <= 0 || C <= 0) return 0;
+  return (unsigned long long)ln_bwd_waves(rows) * 2 * C * sizeof(float);
+}
+
+extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b,
+                                   int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows,
+                                   int C, float *dx32, void *dx16, float *dgamma, float *dbeta, void *workspace,
+                                   unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (rows < 0 || C <= 0) return PCOPS_ERR_INVALID;
+  if (C > 512 * kMaxCh || C % 8) return PCOPS_ERR_UNSUPPORTED;
+  if (!dgamma || !dbeta) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (rows == 0) {
+    if (hipMemsetAsync(dgamma, 0, sizeof(float) * C, s) != hipSuccess ||
+        hipMemsetAsync(dbeta, 0, sizeof(float) * C, s) != hipSuccess)
+      return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!a || !gamma || !mean || !rstd || (!dy32 && !dy16) || (!dx32 && !dx16) || !dt_ok(a_dtype) ||
+      (b && !dt_ok(b_dtype)))
+    return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_layernorm_bwd_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
+  const int waves = ln_bwd_waves(rows);
+  float *part = (float *)workspace;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(waves / 4), dim3(256), 0, s, dy32, (const __bf16 *)dy16, a, a_dtype, b,
+                     b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16, part);
+  hipLaunchKernelGGL(ln_colsum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, part, waves, 2 * C, dgamma, dbeta, C);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}

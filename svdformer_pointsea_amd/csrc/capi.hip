@@ -12,4 +12,4 @@ extern "C" const char *pcops_status_string(int status) {
   }
 }
 
-extern "C" int pcops_abi_version(void) { return 1; }
+extern "C" int pcops_abi_version(void) { return 2; }

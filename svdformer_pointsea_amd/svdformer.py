@@ -19,10 +19,15 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import SDG_Decoder, cross_attention, self_attention
+from .attention import SDG_Decoder, cross_attention, self_attention, to_channels, to_tokens
 from .chamfer3D import chamfer_3DDist
 from .model_utils import fps_subsample, group_local, sample_and_group_knn
 from .pointnet2_utils import furthest_point_sample, gather_operation
+
+
+def _lin(conv, x):
+    """A kernel-size-1 Conv1d applied to token-major (..., C_in) rows as a GEMM."""
+    return F.linear(x, conv.weight.view(conv.weight.shape[0], -1), conv.bias)
 
 
 # ----------------------------------------------------------------- blocks
@@ -301,24 +306,45 @@ class SDG(nn.Module):
         self.cd_distance = chamfer_3DDist()
 
     def forward(self, local_feat, coarse, f_g, partial):
-        batch_size, _, N = coarse.size()
-        F_ = self.conv_x1(self.relu(self.conv_x(coarse)))
-        f_g = self.conv_1(self.relu(self.conv_11(f_g)))
-        F_ = torch.cat([F_, f_g.repeat(1, 1, F_.shape[-1])], dim=1)
+        """Reference signature: (B,C,512), (B,3,N), (B,512,1), (B,3,2048) -> (B,3,N*ratio)."""
+        out = self.forward_tokens(to_tokens(local_feat), coarse.transpose(1, 2).contiguous(), f_g,
+                                  partial.transpose(1, 2).contiguous())
+        return out.transpose(1, 2).contiguous()
+
+    @staticmethod
+    def _decode(dec, x):
+        if isinstance(dec, SDG_Decoder):
+            return dec.forward_tokens(x)
+        s, f = dec.forward_tokens(x)
+        return s + f
+
+    def forward_tokens(self, local_tok, coarse, f_g, partial):
+        """Token-major SDG: local_tok (B,512,C), coarse (B,N,3), f_g (B,512,1),
+        partial (B,2048,3) -> (B,N*ratio,3).  Every 1x1 conv is a GEMM on
+        contiguous rows; the reference's two raw reshapes (SVDFormer.py:77,
+        :92) are reproduced as the equivalent token-major index maps."""
+        B, N, _ = coarse.shape
+        F_ = _lin(self.conv_x1, self.relu(_lin(self.conv_x, coarse)))
+        g = _lin(self.conv_1, self.relu(_lin(self.conv_11, f_g.transpose(1, 2))))
+        F_ = torch.cat([F_, g.expand(B, N, g.shape[-1]).to(F_.dtype)], dim=-1)
         # structure analysis: half Chamfer distance to the partial input
-        half_cd = self.cd_distance(coarse.transpose(1, 2).float().contiguous(),
-                                   partial.transpose(1, 2).float().contiguous())[0] / self.sigma
-        # raw reshape of (B, N, hidden) to (B, hidden, N) (reference quirk, SVDFormer.py:77)
-        embd = self.embedding(half_cd).reshape(batch_size, self.hidden, -1).permute(2, 0, 1)
-        F_Q = self.sa1(F_, embd)
-        F_Q_ = self.decoder1(F_Q)
+        half_cd = self.cd_distance(coarse.float().contiguous(), partial.float().contiguous())[0] / self.sigma
+        # (B,N,hidden).reshape(B,hidden,N).permute(2,0,1) of the reference, token-major
+        pos = self.embedding(half_cd).reshape(B, self.hidden, N).transpose(1, 2)
+        s, f = self.sa1.forward_tokens(F_, pos)
+        F_Q = s + f
+        F_Q_ = self._decode(self.decoder1, F_Q)
         # similarity alignment with the local features
-        local_feat = self.mlpp(local_feat)
-        F_H = self.cross1(F_Q, local_feat)
-        F_H_ = self.decoder2(F_H)
-        F_L = self.conv_delta(self.conv_ps(torch.cat([F_Q_, F_H_], 1)).reshape(batch_size, -1, N * self.ratio))
-        O_L = self.conv_out(self.relu(self.conv_out1(F_L)))
-        return coarse.repeat(1, 1, self.ratio) + O_L
+        local = _lin(self.mlpp.mlp[2], self.mlpp.mlp[1](_lin(self.mlpp.mlp[0], local_tok)))
+        s, f = self.cross1.forward_tokens(F_Q, local)
+        F_H_ = self._decode(self.decoder2, s + f)
+        T = _lin(self.conv_ps, torch.cat([F_Q_.to(F_H_.dtype), F_H_], dim=-1))
+        # (B, C*r, N).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n
+        r = self.ratio
+        F_L = T.reshape(B, N, -1, r).permute(0, 3, 1, 2).reshape(B, r * N, -1)
+        F_L = _lin(self.conv_delta, F_L)
+        O_L = _lin(self.conv_out, self.relu(_lin(self.conv_out1, F_L)))
+        return coarse.repeat(1, r, 1) + O_L
 
 
 class SVFNet(nn.Module):
@@ -397,16 +423,18 @@ class Model(nn.Module):
                 m.to(memory_format=torch.channels_last)
 
     def forward(self, partial, depth):
-        partial = partial.transpose(1, 2).contiguous()
-        feat_g, coarse = self.encoder(partial, depth)
-        local_feat = self.localencoder(partial)
-        coarse_merge = torch.cat([partial, coarse.to(partial.dtype)], dim=2).float().contiguous()
+        partial_cm = partial.transpose(1, 2).contiguous()
+        feat_g, coarse = self.encoder(partial_cm, depth)
+        local_feat = self.localencoder(partial_cm)
+        coarse_merge = torch.cat([partial_cm, coarse.to(partial_cm.dtype)], dim=2).float().contiguous()
         coarse_merge = gather_operation(coarse_merge, furthest_point_sample(coarse_merge.transpose(1, 2).contiguous(),
                                                                             self.merge_points))
-        fine1 = self.refine1(local_feat, coarse_merge, feat_g, partial)
-        fine2 = self.refine2(local_feat, fine1, feat_g, partial)
-        return (coarse.transpose(1, 2).contiguous(), fine1.transpose(1, 2).contiguous(),
-                fine2.transpose(1, 2).contiguous())
+        # the refinement stages run token-major end to end (B, N, C)
+        local_tok = to_tokens(local_feat)
+        partial = partial.contiguous()
+        fine1 = self.refine1.forward_tokens(local_tok, coarse_merge.transpose(1, 2).contiguous(), feat_g, partial)
+        fine2 = self.refine2.forward_tokens(local_tok, fine1, feat_g, partial)
+        return coarse.transpose(1, 2).contiguous(), fine1, fine2
 
 
 # ----------------------------------------------------------------- loss

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     L = ctypes.CDLL(_lib.LIB_PATH)
     for name in _declared():
         assert hasattr(L, name), name
-    assert _lib.lib().pcops_abi_version() == 1
+    assert _lib.lib().pcops_abi_version() == 2
     assert _lib.lib().pcops_status_string(0) == b"ok"
 
 

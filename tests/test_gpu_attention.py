@@ -124,25 +124,116 @@ def test_blocks_match_reference_golden(dev):
         np.testing.assert_allclose(y.cpu().numpy(), g["sav_y"], **tol)
 
 
-def test_block_gradients_match_torch_mha(dev):
-    """self_attention backward through our core == through torch's MHA."""
+def _torch_block(blk, x, pos=None, x2=None):
+    """The reference's self_attention / cross_attention forward
+    (models/model_utils.py:542-617) in plain torch ops, on blk's parameters."""
+    import torch.nn.functional as F
+
+    C = blk.norm13.weight.shape[0]
+    mha = blk.multihead_attn
+
+    def inp(t):
+        t = F.conv1d(t, blk.input_proj.weight, blk.input_proj.bias) if hasattr(blk, "input_proj") else t
+        return F.layer_norm(t.permute(2, 0, 1), (C,), blk.norm13.weight, blk.norm13.bias, blk.norm13.eps)
+
+    s1 = inp(x)
+    kv = s1 if x2 is None else inp(x2)
+    q = s1 if pos is None else s1 + pos
+    k = q if x2 is None else kv
+    a = F.multi_head_attention_forward(q, k, kv, C, mha.num_heads, mha.in_proj_weight, mha.in_proj_bias, None, None,
+                                       False, 0.0, mha.out_proj.weight, mha.out_proj.bias, training=False,
+                                       need_weights=False)[0]
+    s1 = F.layer_norm(s1 + a, (C,), blk.norm12.weight, blk.norm12.bias, blk.norm12.eps)
+    f = blk.linear12(blk.activation1(blk.linear11(s1)))
+    return (s1 + f).permute(1, 2, 0)
+
+
+@pytest.mark.parametrize("kind", ["self", "self_pos", "cross", "woinp"])
+def test_block_gradients_match_torch(dev, kind):
+    """Fused token-major block (packed projections, fused LayerNorm/transpose
+    kernels, MFMA core) == the reference block in torch ops: outputs, input and
+    parameter gradients, fp32."""
     from svdformer_pointsea_amd import attention as A
 
     torch.manual_seed(0)
-    ours = A.self_attention(64, 128, nhead=4).to(dev)
-    ref = torch.nn.MultiheadAttention(128, 4).to(dev)
-    ref.load_state_dict(ours.multihead_attn.state_dict())
-    x = torch.randn(2, 64, 50, device=dev, requires_grad=True)
-    y = ours(x)
-    y.square().sum().backward()
-    g_ours = [p.grad.clone() for p in ours.multihead_attn.parameters()]
-    # same block with torch's MHA swapped in
-    ours.zero_grad()
-    mha = ours.multihead_attn
-    ours.multihead_attn = ref
-    x2 = x.detach().clone().requires_grad_(True)
-    ours(x2).square().sum().backward()
-    for a, p in zip(g_ours, ref.parameters()):
-        torch.testing.assert_close(a, p.grad, rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-4, atol=1e-5)
-    ours.multihead_attn = mha
+    if kind == "cross":
+        blk = A.cross_attention(64, 128, nhead=4).to(dev)
+    elif kind == "woinp":
+        blk = A.self_attention_woinp(128, 128, nhead=4).to(dev)
+    else:
+        blk = A.self_attention(64, 128, nhead=4).to(dev)
+    cin = 128 if kind == "woinp" else 64
+    x = torch.randn(2, cin, 50, device=dev)
+    x2 = torch.randn(2, cin, 37, device=dev) if kind == "cross" else None
+    pos = torch.randn(50, 2, 128, device=dev) if kind == "self_pos" else None
+    ins = [t.clone().requires_grad_(True) for t in (x, x2) if t is not None]
+    y = blk(*ins, pos) if kind != "woinp" else blk(ins[0])
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    g_ours = {n: p.grad.clone() for n, p in blk.named_parameters()}
+    gin_ours = [t.grad.clone() for t in ins]
+    blk.zero_grad()
+    ins2 = [t.detach().clone().requires_grad_(True) for t in ins]
+    y2 = _torch_block(blk, ins2[0], pos, ins2[1] if kind == "cross" else None)
+    (y2 * gy).sum().backward()
+    torch.testing.assert_close(y, y2, rtol=1e-4, atol=2e-5)
+    for a, b in zip(gin_ours, ins2):
+        torch.testing.assert_close(a, b.grad, rtol=1e-4, atol=2e-5)
+    for n, p in blk.named_parameters():
+        torch.testing.assert_close(g_ours[n], p.grad, rtol=1e-4, atol=5e-5, msg=n)
+
+
+def test_block_bf16_autocast_close_to_fp32(dev):
+    """Under bf16 autocast (the training configuration) the fused block stays
+    within bf16 tolerance of its fp32 result, forward and backward."""
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(1)
+    dec = A.SDG_Decoder(256, 32, 8).to(dev)  # head dims 32 / 32
+    x = torch.randn(2, 256, 300, device=dev, requires_grad=True)
+    y = dec(x)
+    y.square().mean().backward()
+    g32 = {n: p.grad.clone() for n, p in dec.named_parameters()}
+    gx = x.grad.clone()
+    dec.zero_grad()
+    x.grad = None
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = dec(x)
+    assert yb.dtype == torch.float32
+    yb.square().mean().backward()
+    assert (yb - y).norm() / y.norm() < 2e-2
+    assert (x.grad - gx).norm() / gx.norm() < 5e-2
+    for n, p in dec.named_parameters():
+        rel = (p.grad - g32[n]).norm() / max(g32[n].norm(), 1e-12)
+        assert rel < 8e-2, (n, rel.item())
+
+
+def test_layernorm_and_transpose_kernels(dev):
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(2)
+    norm = torch.nn.LayerNorm(768).to(dev)
+    with torch.no_grad():
+        norm.weight.normal_()
+        norm.bias.normal_()
+    a = torch.randn(3, 70, 768, device=dev, requires_grad=True)
+    b = torch.randn(3, 70, 768, device=dev).to(torch.bfloat16).requires_grad_(True)
+    y, _ = A.layer_norm(norm, a, b)
+    ref = torch.nn.functional.layer_norm(a + b.float(), (768,), norm.weight, norm.bias, norm.eps)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    ga, gb, gw = a.grad.clone(), b.grad.clone(), norm.weight.grad.clone()
+    a.grad = b.grad = None
+    norm.zero_grad()
+    (torch.nn.functional.layer_norm(a + b.float(), (768,), norm.weight, norm.bias, norm.eps) * g).sum().backward()
+    torch.testing.assert_close(ga, a.grad, rtol=1e-4, atol=1e-5)
+    assert gb.dtype == torch.bfloat16
+    torch.testing.assert_close(gb.float(), b.grad.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(gw, norm.weight.grad, rtol=1e-4, atol=1e-4)
+    # (B, C, L) <-> (B, L, C), ragged tiles, with an add and a dtype change
+    x = torch.randn(2, 130, 67, device=dev)
+    t = A.to_tokens(x)
+    torch.testing.assert_close(t, x.transpose(1, 2))
+    z = A.to_channels(t, t.to(torch.bfloat16), torch.bfloat16)
+    torch.testing.assert_close(z.float(), (x + x.to(torch.bfloat16).float()).to(torch.bfloat16).float())
