@@ -1,0 +1,119 @@
+"""Training losses and evaluation metrics of the reference on libpcops:
+utils/loss_utils.py:10-155 and metrics/CD/fscore.py:3-16.
+
+  chamfer / chamfer_sqrt / chamfer_single_side(_sqrt)    Chamfer losses
+  get_loss / get_loss_PM                                 train_pcn / PointSea losses
+  calc_cd                                                CD-L1 (cd_p), CD-L2 (cd_t), F-score
+  calc_dcd                                               density-aware Chamfer
+  fscore                                                 F-score on squared distances
+Names, arguments and return structures are the reference's.  The
+nearest-neighbour search is the Chamfer kernel (csrc/chamfer.hip, both
+directions in one launch); what follows it are the same reductions, in the
+same floating-point order, as the reference's torch expressions.
+"""
+import torch
+
+from . import chamfer3D
+from .model_utils import fps_subsample
+
+_nn = chamfer3D.chamfer_3DDist()
+
+
+def _means(p1, p2, root):
+    d1, d2, _, _ = _nn(p1, p2)
+    if root:
+        d1, d2 = torch.sqrt(d1), torch.sqrt(d2)
+    return torch.mean(d1), torch.mean(d2)
+
+
+def chamfer(p1, p2):
+    m1, m2 = _means(p1, p2, False)
+    return m1 + m2
+
+
+def chamfer_sqrt(p1, p2):
+    m1, m2 = _means(p1, p2, True)
+    return (m1 + m2) / 2
+
+
+def chamfer_single_side(pcd1, pcd2):
+    return _means(pcd1, pcd2, False)[0]
+
+
+def chamfer_single_side_sqrt(pcd1, pcd2):
+    return _means(pcd1, pcd2, True)[0]
+
+
+def _stage_losses(pcds_pred, gt, CD):
+    """CD of (coarse, fine1, fine2) against gt FPS-subsampled to each size."""
+    Pc, P1, P2 = pcds_pred
+    gt_1 = fps_subsample(gt, P1.shape[1])
+    gt_c = fps_subsample(gt_1, Pc.shape[1])
+    return [CD(Pc, gt_c), CD(P1, gt_1), CD(P2, gt)]
+
+
+def get_loss(pcds_pred, gt, sqrt=True, alpha1=1, alpha2=1):
+    """loss_utils.py:33-58 -> (cdc + alpha1*cd1 + alpha2*cd2, [cdc, cd1, cd2])."""
+    cdc, cd1, cd2 = _stage_losses(pcds_pred, gt, chamfer_sqrt if sqrt else chamfer)
+    return cdc + alpha1 * cd1 + alpha2 * cd2, [cdc, cd1, cd2]
+
+
+def get_loss_PM(pcds_pred, partial, gt, sqrt=True):
+    """loss_utils.py:60-82: get_loss + single-sided partial -> fine2 matching."""
+    cdc, cd1, cd2 = _stage_losses(pcds_pred, gt, chamfer_sqrt if sqrt else chamfer)
+    pm = (chamfer_single_side_sqrt if sqrt else chamfer_single_side)(partial, pcds_pred[2])
+    return cdc + cd1 + cd2 + pm, [cdc, cd1, cd2]
+
+
+def fscore(dist1, dist2, threshold=0.0001):
+    """(f1, precision_1, precision_2) per sample; dist1/dist2 are SQUARED."""
+    p1 = torch.mean((dist1 < threshold).float(), dim=1)
+    p2 = torch.mean((dist2 < threshold).float(), dim=1)
+    f1 = 2 * p1 * p2 / (p1 + p2)
+    f1[torch.isnan(f1)] = 0
+    return f1, p1, p2
+
+
+def calc_cd(output, gt, calc_f1=False, return_raw=False, normalize=False, separate=False):
+    """Per-sample [cd_p (CD-L1), cd_t (CD-L2)] (+ f1) (+ dist1, dist2, idx1, idx2).
+    Distances are gt -> output first, as loss_utils.py:98-115; `normalize` is
+    accepted and unused there too."""
+    dist1, dist2, idx1, idx2 = chamfer3D.chamfer_3DDist()(gt, output)
+    l1 = [torch.sqrt(d).mean(1) for d in (dist1, dist2)]
+    l2 = [d.mean(1) for d in (dist1, dist2)]
+    if separate:
+        res = [torch.cat([v.unsqueeze(0) for v in l1]), torch.cat([v.unsqueeze(0) for v in l2])]
+    else:
+        res = [(l1[0] + l1[1]) / 2, l2[0] + l2[1]]
+    if calc_f1:
+        res.append(fscore(dist1, dist2)[0])
+    if return_raw:
+        res.extend([dist1, dist2, idx1, idx2])
+    return res
+
+
+def _density_term(dist, idx, n_targets, alpha, n_lambda, frac):
+    """mean_i (1 - exp(-alpha d_i) / (n_hits(idx_i)^lambda + 1e-6) * frac)."""
+    hits = torch.zeros(idx.shape[0], n_targets, dtype=idx.dtype, device=idx.device)
+    hits.scatter_add_(1, idx.long(), torch.ones_like(idx))
+    w = hits.gather(1, idx.long()).float().detach() ** n_lambda
+    w = (w + 1e-6) ** (-1) * frac
+    return (1 - torch.exp(-dist * alpha) * w).mean(dim=1)
+
+
+def calc_dcd(x, gt, alpha=1000, n_lambda=1, return_raw=False, non_reg=False):
+    """Density-aware Chamfer distance -> [dcd, cd_p, cd_t] (+ raw)."""
+    x, gt = x.float(), gt.float()
+    n_x, n_gt = x.shape[1], gt.shape[1]
+    assert x.shape[0] == gt.shape[0]
+    f12, f21 = n_x / n_gt, n_gt / n_x
+    if non_reg:
+        f12, f21 = max(1, f12), max(1, f21)
+    cd_p, cd_t, dist1, dist2, idx1, idx2 = calc_cd(x, gt, return_raw=True)
+    # dist1/idx1: every gt point's nearest x; dist2/idx2: every x's nearest gt
+    loss = (_density_term(dist1, idx1, n_x, alpha, n_lambda, f21) +
+            _density_term(dist2, idx2, n_gt, alpha, n_lambda, f12)) / 2
+    res = [loss, cd_p, cd_t]
+    if return_raw:
+        res.extend([dist1, dist2, idx1, idx2])
+    return res

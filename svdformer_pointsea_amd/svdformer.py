@@ -438,26 +438,8 @@ class Model(nn.Module):
 
 
 # ----------------------------------------------------------------- loss
-_chamfer = chamfer_3DDist()
-
-
-def chamfer_sqrt(p1, p2):
-    """utils/loss_utils.py:15-19: (mean sqrt d1 + mean sqrt d2) / 2."""
-    d1, d2, _, _ = _chamfer(p1.float(), p2.float())
-    return (torch.mean(torch.sqrt(d1)) + torch.mean(torch.sqrt(d2))) / 2
-
-
-def get_loss(pcds_pred, gt, sqrt=True, alpha1=1, alpha2=1):
-    """utils/loss_utils.py:33-58 (sqrt=True path used by train_pcn.py:111)."""
-    if not sqrt:
-        raise NotImplementedError("train_pcn uses sqrt=True")
-    Pc, P1, P2 = pcds_pred
-    gt_1 = fps_subsample(gt, P1.shape[1])
-    gt_c = fps_subsample(gt_1, Pc.shape[1])
-    cdc = chamfer_sqrt(Pc, gt_c)
-    cd1 = chamfer_sqrt(P1, gt_1)
-    cd2 = chamfer_sqrt(P2, gt)
-    return cdc + alpha1 * cd1 + alpha2 * cd2, [cdc, cd1, cd2]
+# get_loss / chamfer_sqrt live in metrics.py (utils/loss_utils.py); re-exported here
+from .metrics import chamfer_sqrt, get_loss  # noqa: E402,F401
 
 
 class PCNConfig:
