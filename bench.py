@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="issue every launch from Python (no HIP graph)")
+    ap.add_argument("--timing-steps", type=int, default=2, help="eager steps timed per launch (graph mode)")
     return ap.parse_args()
 
 
@@ -79,15 +81,32 @@ def synth_pcn(B, seed, device):
     return partial.contiguous().to(device), gt.contiguous().to(device)
 
 
-def wrap_ddp(model, device_ids):
-    """Batch-partitioned data parallelism: the gradient all-reduce (RCCL on
-    GPUs, gloo in the CPU tests) is the only collective of the step.  64 MB
-    buckets -> 4 ring all-reduces for the 232 MB of fp32 gradients; static
-    graph because the if_bn=False Conv2d blocks own BatchNorms that never get
-    a gradient; BN statistics stay per replica (broadcast_buffers=False)."""
-    return torch.nn.parallel.DistributedDataParallel(
-        model, device_ids=device_ids, broadcast_buffers=False, gradient_as_bucket_view=True, bucket_cap_mb=64,
-        static_graph=True)
+class GradBucket:
+    """All parameter gradients as views of ONE flat fp32 buffer.
+
+    Batch-partitioned data parallelism needs exactly one exchange per step:
+    the gradient all-reduce, here a single RCCL all_reduce over the whole
+    232 MB bucket (ring, one call, no per-parameter launches).  The views keep
+    each parameter's strides (channels_last conv weights), so the fused Adam
+    kernel sees grads laid out like their params.  Parameters that never get
+    a gradient (the BatchNorms of the if_bn=False Conv2d blocks) keep a zero
+    one, which leaves them unchanged under Adam, as a None grad would."""
+
+    def __init__(self, params, device):
+        params = list(params)
+        self.flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=device)
+        off = 0
+        for p in params:
+            p.grad = self.flat[off:off + p.numel()].as_strided(p.shape, p.stride())
+            off += p.numel()
+
+    def zero(self):
+        self.flat.zero_()
+
+    def allreduce(self, world):
+        if world > 1:
+            dist.all_reduce(self.flat)
+            self.flat.mul_(1.0 / world)
 
 
 # ------------------------------------------------------------------ roofline model
@@ -217,39 +236,82 @@ def main():
     torch.manual_seed(0)  # identical init on every rank
     model = Model(PCNConfig).to(device)
     nparams = sum(p.numel() for p in model.parameters())
-    if world > 1:
-        model = wrap_ddp(model, [local])
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999), weight_decay=0, fused=True)
+    bucket = GradBucket(model.parameters(), device)
+    use_graph = not args.no_graph
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999), weight_decay=0, fused=True,
+                           capturable=use_graph)
     render = PCViews(TRANS=-PCNConfig.NETWORK.view_distance, RESOLUTION=224)
     partial, gt = synth_pcn(args.batch, 1000 + rank, device)
     loss_acc = torch.zeros((), device=device)
     amp = not args.fp32
 
-    def step():
-        nonlocal loss_acc
+    def fwd_bwd():
+        bucket.zero()
         depth = render.get_img(partial).unsqueeze(1)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=not use_graph):
             pcds = model(partial, depth)
             loss, _ = get_loss(pcds, gt)
-        opt.zero_grad(set_to_none=True)
         loss.backward()
-        opt.step()
-        loss_acc = loss_acc + loss.detach()  # logged without a host sync
+        loss_acc.add_(loss.detach())  # logged without a host sync
 
-    for _ in range(args.warmup):
-        step()
-    if not args.no_kernel_timing:
-        _lib.KernelTimer.enable()
+    def eager_step():
+        fwd_bwd()
+        bucket.allreduce(world)
+        opt.step()
+
+    if use_graph:
+        # The host cannot issue the ~3k launches of a step faster than the GPU
+        # runs them (host_issue_ms_per_step), so the step is captured once
+        # into two HIP graphs (forward+backward, Adam) after eager warm-up on
+        # a side stream (MIOpen algorithm search, lazy state); the gradient
+        # all-reduce stays an eager RCCL call between the two replays.
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(args.warmup, 2)):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            fwd_bwd()
+        with torch.cuda.graph(g_opt):
+            opt.step()
+
+        def step():
+            g_fb.replay()
+            bucket.allreduce(world)
+            g_opt.replay()
+        span_steps = args.timing_steps
+    else:
+        step = eager_step
+        for _ in range(args.warmup):
+            step()
+        if not args.no_kernel_timing:
+            _lib.KernelTimer.enable()
+        span_steps = args.steps
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host = 0.0  # time the host spends issuing a step (launches are asynchronous)
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         step()
+        host += time.perf_counter() - h0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if use_graph and not args.no_kernel_timing:
+        # ROCm torch refuses timing events inside a captured graph ("External
+        # events are disallowed in rocm"), so the per-launch HIP events come
+        # from eager steps of the same work right after the timed replays.
+        _lib.KernelTimer.enable()
+        for _ in range(args.timing_steps):
+            eager_step()
+        torch.cuda.synchronize()
     spans = _lib.KernelTimer.spans or {}
     _lib.KernelTimer.disable()
     if world > 1:
@@ -271,6 +333,10 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
+            "host_issue_ms_per_step": host * 1e3 / args.steps,
+            "execution": "hip_graph" if use_graph else "eager",
+            "kernel_timing": ("HIP events per libpcops launch, %d eager steps after the timed graph replays"
+                              % args.timing_steps) if use_graph else "HIP events per libpcops launch, timed steps",
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -296,9 +362,9 @@ def main():
                 out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) /
                                                          sum(r["ms"] for r in group), 4)
             step_ms = elapsed * 1e3 / args.steps
-            out["kernels"] = {k: {"launches_per_step": r["launches"] / args.steps,
-                                  "ms_per_step": round(r["ms"] / args.steps, 4),
-                                  "share": round(r["ms"] / args.steps / step_ms, 4),
+            out["kernels"] = {k: {"launches_per_step": r["launches"] / span_steps,
+                                  "ms_per_step": round(r["ms"] / span_steps, 4),
+                                  "share": round(r["ms"] / span_steps / step_ms, 4),
                                   **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {})}
                               for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
         if world == 1 and not args.no_cpu_baseline:

@@ -420,6 +420,18 @@ __device__ __forceinline__ void v_product(f32x16 (&Y)[D / 32], const __bf16 *lds
 #endif
 }
 
+// XCD-aware block order: the hardware hands consecutive workgroups to the 8
+// XCDs round-robin, so the row blocks of one (batch, head) would land on 8
+// different L2s and fetch that head's K/V (or Q/dO) 8 times.  Remap the
+// linear id so each XCD gets a contiguous range of (head, row-block) pairs.
+__device__ __forceinline__ void xcd_block(int &rb, int &bh) {
+  const int nrb = gridDim.x, total = gridDim.x * gridDim.y;
+  int L = blockIdx.x + nrb * blockIdx.y;
+  if ((total & 7) == 0) L = (L & 7) * (total >> 3) + (L >> 3);
+  rb = L % nrb;
+  bh = L / nrb;
+}
+
 template <int D, int NW>
 struct Fwd2Cfg {
   static constexpr int kThr = NW * 64;
@@ -470,9 +482,10 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
   extern __shared__ __attribute__((aligned(16))) unsigned char fwd2_smem[];
   __bf16 *sk = reinterpret_cast<__bf16 *>(fwd2_smem);
   __bf16 *sv = sk + 2 * C::kKBuf;
-  const int bh = blockIdx.y;
+  int rb, bh;
+  xcd_block(rb, bh);
   const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
-  const int q0 = blockIdx.x * (NW * 32) + w * 32;
+  const int q0 = rb * (NW * 32) + w * 32;
   const int qi = q0 + (l & 31);
   bf16x8 qf[D / 16];
   {
@@ -563,9 +576,10 @@ __global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restr
   extern __shared__ __attribute__((aligned(16))) unsigned char bwd2_smem[];
   __bf16 *sk = reinterpret_cast<__bf16 *>(bwd2_smem);
   __bf16 *sv = sk + 2 * C::kKBuf;
-  const int bh = blockIdx.y;
+  int rb, bh;
+  xcd_block(rb, bh);
   const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
-  const int q0 = blockIdx.x * (NW * 32) + w * 32;
+  const int q0 = rb * (NW * 32) + w * 32;
   const int qi = q0 + (l & 31);
   const bool qv = qi < Lq;
   bf16x8 qf[D / 16], gf[D / 16];
@@ -638,9 +652,10 @@ __global__ __launch_bounds__(NW * 64) void attn_dkv2_kernel(const __bf16 *__rest
   __bf16 *sg = sq + 2 * C::kKBuf;
   float *slse = reinterpret_cast<float *>(sg + 2 * C::kVBuf);  // [2][64]
   float *sdl = slse + 2 * kKT;                                  // [2][64]
-  const int bh = blockIdx.y;
+  int rb, bh;
+  xcd_block(rb, bh);
   const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
-  const int k0w = blockIdx.x * (NW * 32) + w * 32;
+  const int k0w = rb * (NW * 32) + w * 32;
   const int ki = k0w + (l & 31);
   const bool kv = ki < Lk;
   bf16x8 kf[D / 16], vf[D / 16];

@@ -149,9 +149,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a,
   }
 }
 
-// One wave per row, grid-stride; dgamma / dbeta partial sums per wave go to
-// a [waves][2][C] scratch (plain stores: thousands of waves atomically adding
-// into the same 2*C floats would serialise), reduced by ln_colsum_kernel.
+// Each wave owns kRowsPerWave consecutive rows (one at a time, full row in
+// registers); the block's dgamma / dbeta partial sums are reduced through LDS
+// and written once per block to a [blocks][2C] scratch (plain stores --
+// thousands of waves atomically adding into the same 2C floats serialise),
+// then summed by ln_colsum_kernel.
+constexpr int kRowsPerWave = 4;
+constexpr int kRowsPerBlock = 4 * kRowsPerWave;
+
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g32, const __bf16 *__restrict__ g16,
                                                      const void *__restrict__ a, int adt, const void *__restrict__ b,
                                                      int bdt, const float *__restrict__ gamma,
@@ -159,51 +164,51 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
                                                      const float *__restrict__ rstd_in, int rows, int C,
                                                      float *__restrict__ dx32, __bf16 *__restrict__ dx16,
                                                      float *__restrict__ part) {
-  const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int nwaves = gridDim.x * 4;
+  __shared__ float red[4][2 * 1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = C >> 3;
   V8 dg[kMaxCh], db[kMaxCh];
 #pragma unroll
   for (int i = 0; i < kMaxCh; ++i)
 #pragma unroll
     for (int k = 0; k < 8; ++k) dg[i].v[k] = db[i].v[k] = 0.f;
-  for (int row = wave; row < rows; row += nwaves) {
+  const int r0 = blockIdx.x * kRowsPerBlock + w * kRowsPerWave;
+  for (int row = r0; row < r0 + kRowsPerWave && row < rows; ++row) {
     const long long base = (long long)row * C;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    V8 xh[kMaxCh], g[kMaxCh];
+    V8 xh[kMaxCh], dy[kMaxCh];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < kMaxCh; ++i) {
       const int ch = lane + 64 * i;
       if (ch < nch) {
-        V8 x, dy, t;
-        ld8(x, a, adt, base + 8 * ch);
+        V8 t;
+        ld8(xh[i], a, adt, base + 8 * ch);
         if (b) {
           ld8(t, b, bdt, base + 8 * ch);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) x.v[k] += t.v[k];
+          for (int k = 0; k < 8; ++k) xh[i].v[k] += t.v[k];
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dy.v[k] = 0.f;
+        for (int k = 0; k < 8; ++k) dy[i].v[k] = 0.f;
         if (g32) {
           ld8(t, g32, 0, base + 8 * ch);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) dy.v[k] += t.v[k];
+          for (int k = 0; k < 8; ++k) dy[i].v[k] += t.v[k];
         }
         if (g16) {
           ld8(t, g16, 1, base + 8 * ch);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) dy.v[k] += t.v[k];
+          for (int k = 0; k < 8; ++k) dy[i].v[k] += t.v[k];
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          xh[i].v[k] = (x.v[k] - mean) * rstd;
-          dg[i].v[k] = __builtin_fmaf(dy.v[k], xh[i].v[k], dg[i].v[k]);
-          db[i].v[k] += dy.v[k];
-          g[i].v[k] = dy.v[k] * gamma[8 * ch + k];
-          sg += g[i].v[k];
-          sgx = __builtin_fmaf(g[i].v[k], xh[i].v[k], sgx);
+          xh[i].v[k] = (xh[i].v[k] - mean) * rstd;
+          dg[i].v[k] = __builtin_fmaf(dy[i].v[k], xh[i].v[k], dg[i].v[k]);
+          db[i].v[k] += dy[i].v[k];
+          const float g = dy[i].v[k] * gamma[8 * ch + k];
+          sg += g;
+          sgx = __builtin_fmaf(g, xh[i].v[k], sgx);
         }
       }
     }
@@ -215,46 +220,58 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
       if (ch < nch) {
         V8 dx;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dx.v[k] = rstd * (g[i].v[k] - mg - xh[i].v[k] * mgx);
+        for (int k = 0; k < 8; ++k)
+          dx.v[k] = rstd * (dy[i].v[k] * gamma[8 * ch + k] - mg - xh[i].v[k] * mgx);
         if (dx32) st8_f32(dx32, base + 8 * ch, dx);
         if (dx16) st8_bf16(dx16, base + 8 * ch, dx);
       }
     }
   }
-  float *pw = part + (long long)wave * 2 * C;
 #pragma unroll
   for (int i = 0; i < kMaxCh; ++i) {
     const int ch = lane + 64 * i;
-    if (ch < nch) {
-      st8_f32(pw, 8 * ch, dg[i]);
-      st8_f32(pw + C, 8 * ch, db[i]);
-    }
+    if (ch < nch)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[w][8 * ch + k] = dg[i].v[k];
+        red[w][C + 8 * ch + k] = db[i].v[k];
+      }
   }
+  __syncthreads();
+  float *pb = part + (long long)blockIdx.x * 2 * C;
+  for (int c = threadIdx.x; c < 2 * C; c += 256) pb[c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
 }
 
-// out[c] = sum_w part[w][c] for 2*C columns (dgamma then dbeta)
-__global__ __launch_bounds__(256) void ln_colsum_kernel(const float *__restrict__ part, int waves, int C2,
-                                                        float *__restrict__ dgamma, float *__restrict__ dbeta, int C) {
+// dgamma / dbeta = column sums of the [blocks][2C] partials, deterministic:
+// grid (2C/64, slices) sums row slices into [slices][2C] (4 waves interleaved
+// over rows), then a (2C/64, 1) launch of the same kernel sums the slices.
+constexpr int kColSlices = 64;
+
+__global__ __launch_bounds__(256) void ln_colsum_kernel(const float *__restrict__ part, int nrows, int C2,
+                                                        float *__restrict__ out, float *__restrict__ dgamma,
+                                                        float *__restrict__ dbeta, int C) {
   __shared__ float red[4][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r = threadIdx.x >> 6;
+  const int per = (nrows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(nrows, r0 + per);
   float s = 0.f;
   if (col < C2)
-    for (int w = r; w < waves; w += 4) s += part[(long long)w * C2 + col];
+    for (int w = r0 + r; w < r1; w += 4) s += part[(long long)w * C2 + col];
   red[r][threadIdx.x & 63] = s;
   __syncthreads();
   if (r == 0 && col < C2) {
     const float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
-    if (col < C)
+    if (out)
+      out[(long long)blockIdx.y * C2 + col] = t;
+    else if (col < C)
       dgamma[col] = t;
     else
       dbeta[col - C] = t;
   }
 }
 
-constexpr int kLnBwdWaves = 1024;
-
-int ln_bwd_waves(int rows) { return ((rows < kLnBwdWaves ? rows : kLnBwdWaves) + 3) / 4 * 4; }
+int ln_bwd_blocks(int rows) { return (rows + kRowsPerBlock - 1) / kRowsPerBlock; }
 
 bool dt_ok(int dt) { return dt == 0 || dt == 1; }
 
@@ -289,7 +306,7 @@ extern "C" int pcops_layernorm_fwd(const void *a, int a_dtype, const void *b, in
 
 extern "C" unsigned long long pcops_layernorm_bwd_workspace_bytes(int rows, int C) {
   if (rows <= 0 || C <= 0) return 0;
-  return (unsigned long long)ln_bwd_waves(rows) * 2 * C * sizeof(float);
+  return (unsigned long long)(ln_bwd_blocks(rows) + kColSlices) * 2 * C * sizeof(float);
 }
 
 extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b,
@@ -310,11 +327,16 @@ extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const vo
       (b && !dt_ok(b_dtype)))
     return PCOPS_ERR_INVALID;
   if (!workspace || workspace_bytes < pcops_layernorm_bwd_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
-  const int waves = ln_bwd_waves(rows);
+  const int blocks = ln_bwd_blocks(rows);
   float *part = (float *)workspace;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(waves / 4), dim3(256), 0, s, dy32, (const __bf16 *)dy16, a, a_dtype, b,
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, s, dy32, (const __bf16 *)dy16, a, a_dtype, b,
                      b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16, part);
-  hipLaunchKernelGGL(ln_colsum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, part, waves, 2 * C, dgamma, dbeta, C);
+  float *slice = part + (size_t)blocks * 2 * C;
+  const int slices = blocks < kColSlices ? blocks : kColSlices;
+  hipLaunchKernelGGL(ln_colsum_kernel, dim3((2 * C + 63) / 64, slices), dim3(256), 0, s, part, blocks, 2 * C, slice,
+                     nullptr, nullptr, C);
+  hipLaunchKernelGGL(ln_colsum_kernel, dim3((2 * C + 63) / 64, 1), dim3(256), 0, s, slice, slices, 2 * C, nullptr,
+                     dgamma, dbeta, C);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

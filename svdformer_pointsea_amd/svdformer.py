@@ -368,15 +368,18 @@ class SVFNet(nn.Module):
             nn.BatchNorm2d(16, eps=1e-05, momentum=0.1, affine=True, track_running_stats=True),
             nn.ReLU(inplace=True), *res_layers, Squeeze())
         self.posmlp = MLP_CONV(3, [64, 256])
+        d = self.view_distance
+        # the three camera positions (SVDFormer.py:153), a buffer so the forward
+        # issues no host->device copy (graph-capturable); not in the state_dict
+        self.register_buffer("view_point", torch.tensor([0, 0, -d, -d, 0, 0, 0, d, 0], dtype=torch.float32)
+                             .view(-1, 3, 3).permute(0, 2, 1).contiguous(), persistent=False)
 
     def forward(self, points, depth):
         batch_size, _, N = points.size()
         depth = depth.contiguous(memory_format=torch.channels_last)
         f_v = self.img_feature_extractor(depth).view(batch_size, 3, -1).transpose(1, 2).contiguous()
         f_p = self.point_feature_extractor(points)
-        d = self.view_distance
-        view_point = torch.tensor([0, 0, -d, -d, 0, 0, 0, d, 0], dtype=torch.float32, device=depth.device)
-        view_point = view_point.view(-1, 3, 3).permute(0, 2, 1).expand(batch_size, 3, 3)
+        view_point = self.view_point.expand(batch_size, 3, 3)
         view_feature = self.posmlp(view_point).permute(2, 0, 1)
         f_v_ = self.viewattn(torch.cat([f_v, f_p.repeat(1, 1, f_v.size(2))], 1), view_feature)
         f_v_ = F.adaptive_max_pool1d(f_v_, 1)

@@ -1,8 +1,10 @@
 """World-size-2 gloo run of bench.py's data-parallel path on CPU.
 
 Each rank runs the real SVDFormer PCN step on its own sample (point ops on
-the oracle CPU path) under bench.wrap_ddp; the all-reduced gradients must be
-identical on both ranks and equal the mean of the ranks' local gradients."""
+the oracle CPU path) with bench.GradBucket: gradients accumulate into one flat
+buffer whose all-reduce is the step's only collective.  After it, the
+gradients must be identical on both ranks and equal the mean of the ranks'
+local gradients, and one Adam step must leave identical weights."""
 import os
 import socket
 
@@ -22,32 +24,35 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from bench import synth_pcn, wrap_ddp
+    from bench import GradBucket, synth_pcn
     from oracle.cpu_path import cpu_ops, depth_images
     from svdformer_pointsea_amd.render import PCViews
     from svdformer_pointsea_amd.svdformer import Model, PCNConfig, get_loss
 
     torch.manual_seed(0)
-    local = Model(PCNConfig)
-    ddp = wrap_ddp(Model(PCNConfig), None)
-    ddp.module.load_state_dict(local.state_dict())
+    model = Model(PCNConfig)
+    bucket = GradBucket(model.parameters(), "cpu")
     partial, gt = synth_pcn(1, 1000 + rank, "cpu")
     render = PCViews(TRANS=-0.7, RESOLUTION=224)
     with cpu_ops():
         depth = depth_images(render, partial).unsqueeze(1)
-        for m in (local, ddp):
-            loss, _ = get_loss(m(partial, depth), gt)
-            loss.backward()
-    names = [n for n, p in local.named_parameters() if p.grad is not None]
-    g_local = torch.cat([dict(local.named_parameters())[n].grad.flatten() for n in names])
-    g_ddp = torch.cat([dict(ddp.module.named_parameters())[n].grad.flatten() for n in names])
-    mean_local = g_local.clone()
+        bucket.zero()
+        loss, _ = get_loss(model(partial, depth), gt)
+        loss.backward()
+    local = bucket.flat.clone()
+    bucket.allreduce(world)
+    mean_local = local.clone()
     dist.all_reduce(mean_local)
     mean_local /= world
-    other = g_ddp.clone()
+    other = bucket.flat.clone()
     dist.broadcast(other, src=0)
-    out[rank] = (float((g_ddp - mean_local).abs().max()), float((g_ddp - other).abs().max()),
-                 float(g_local.abs().max()))
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    opt.step()
+    w = torch.cat([p.detach().flatten() for p in model.parameters()])
+    w0 = w.clone()
+    dist.broadcast(w0, src=0)
+    out[rank] = (float((bucket.flat - mean_local).abs().max()), float((bucket.flat - other).abs().max()),
+                 float(local.abs().max()), float((w - w0).abs().max()))
     dist.destroy_process_group()
 
 
@@ -59,6 +64,6 @@ def test_ddp_gloo_world2():
         mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
         res = dict(out)
     for rank in range(world):
-        diff_mean, diff_ranks, scale = res[rank]
-        assert diff_ranks == 0.0
+        diff_mean, diff_ranks, scale, diff_w = res[rank]
+        assert diff_ranks == 0.0 and diff_w == 0.0
         assert diff_mean <= 1e-6 * max(scale, 1.0)
