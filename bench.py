@@ -50,7 +50,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32, help="samples per GPU")
+    ap.add_argument("--model", choices=("svdformer", "pointsea"), default="svdformer",
+                    help="svdformer: PCN train step (configs[2]/[3], the headline); pointsea: ShapeNet-55 "
+                         "train step with the PCViews_Real renderer (configs[4])")
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (32 PCN, 16 ShapeNet-55)")
     ap.add_argument("--fp32", action="store_true", help="no bf16 autocast (configs[1] numerics)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -78,6 +81,32 @@ def synth_pcn(B, seed, device):
         vis = gt[b][(d[b] @ (view[b] / view[b].norm())) > 0]
         pick = torch.randint(0, vis.shape[0], (2048,), generator=g)
         partial[b] = vis[pick]
+    return partial.contiguous().to(device), gt.contiguous().to(device)
+
+
+def synth_55(B, seed, device, n_gt=8192):
+    """ShapeNet-55-shaped synthetic batch: gt (B,8192,3) random rotated
+    ellipsoid surfaces normalised like the loader's pc_norm (centroid at 0,
+    max radius 1); partial (B,2048,3) = gt minus the points nearest a random
+    unit-sphere centre (a quarter to three quarters of them, as
+    core/train_55.py:150), randomly resampled to 2048.  The train step
+    re-derives its own partial on the device each step with
+    data.seprate_point_cloud, as the reference's loop does."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    d = torch.randn(B, n_gt, 3, generator=g)
+    d = d / d.norm(dim=-1, keepdim=True)
+    axes = 0.3 + 0.7 * torch.rand(B, 1, 3, generator=g)
+    q, _ = torch.linalg.qr(torch.randn(B, 3, 3, generator=g))
+    gt = torch.bmm(d * axes, q)
+    gt = gt - gt.mean(dim=1, keepdim=True)
+    gt = gt / gt.norm(dim=-1).amax(dim=1).view(B, 1, 1)
+    partial = torch.empty(B, 2048, 3)
+    for b in range(B):
+        c = torch.randn(1, 3, generator=g)
+        c = c / c.norm()
+        ncrop = int(torch.randint(n_gt // 4, 3 * n_gt // 4 + 1, (1,), generator=g))
+        keep = torch.argsort((gt[b] - c).norm(dim=-1))[ncrop:]
+        partial[b] = gt[b][keep[torch.randint(0, keep.numel(), (2048,), generator=g)]]
     return partial.contiguous().to(device), gt.contiguous().to(device)
 
 
@@ -179,24 +208,76 @@ def kernel_table(spans):
     return rows
 
 
+# ------------------------------------------------------------------ workloads
+class Workload:
+    """One of the two train steps: the reference loop it restates, its model,
+    renderer, loss and optimizer."""
+
+    def __init__(self, name):
+        self.name = name
+        if name == "svdformer":   # core/train_pcn.py:101-134
+            from svdformer_pointsea_amd.render import PCViews
+            from svdformer_pointsea_amd.svdformer import Model, PCNConfig
+            self.Model, self.cfg, self.batch, self.n_out = Model, PCNConfig, 32, 16384
+            self.render = PCViews(TRANS=-PCNConfig.NETWORK.view_distance, RESOLUTION=224)
+            self.synth = synth_pcn
+            self.metric = "train-step samples/sec (PCN, B=32, 2048->16384 pts)"
+            self.desc = "SVDFormer PCN train step: render + fwd + get_loss + bwd + Adam"
+        else:                      # core/train_55.py:141-181 with models_PointSea/PointSea.py
+            from svdformer_pointsea_amd.pointsea import Config55, Model
+            from svdformer_pointsea_amd.render import PCViews_Real
+            self.Model, self.cfg, self.batch, self.n_out = Model, Config55, 16, 8192
+            self.render = PCViews_Real(TRANS=-Config55.NETWORK.view_distance)
+            self.synth = synth_55
+            self.metric = "train-step samples/sec (PointSea ShapeNet-55, B=16, 2048->8192 pts)"
+            self.desc = ("PointSea ShapeNet-55 train step: seprate_point_cloud + PCViews_Real render + fwd + "
+                         "get_loss_PM + bwd + AdamW")
+
+    def optimizer(self, params, **kw):
+        if self.name == "svdformer":   # train_pcn.py:57-60
+            return torch.optim.Adam(params, lr=1e-4, betas=(0.9, 0.999), weight_decay=0, **kw)
+        return torch.optim.AdamW(params, lr=1e-4, weight_decay=0.0005, **kw)   # train_55.py:86-88
+
+    def images(self, partial, cpu=False):
+        if cpu:
+            from oracle.cpu_path import depth_images, real_images
+            if self.name == "svdformer":
+                return depth_images(self.render, partial).unsqueeze(1)
+            return real_images(self.render, partial)
+        img = self.render.get_img(partial)
+        return img.unsqueeze(1) if self.name == "svdformer" else img
+
+    def inputs(self, partial, gt, generator=None):
+        """The partial cloud the step sees: the loader's for PCN; for ShapeNet-55
+        re-cropped from gt on the device every step (train_55.py:150)."""
+        if self.name == "svdformer" or generator is None:
+            return partial
+        from svdformer_pointsea_amd.data import seprate_point_cloud
+        n = gt.shape[1]
+        return seprate_point_cloud(gt, n, [n // 4, 3 * n // 4], generator=generator)[0]
+
+    def loss(self, pcds, partial, gt):
+        from svdformer_pointsea_amd.metrics import get_loss, get_loss_PM
+        if self.name == "svdformer":
+            return get_loss(pcds, gt, sqrt=True)[0]
+        return get_loss_PM(pcds, partial, gt, sqrt=False)[0]
+
+
 # ------------------------------------------------------------------ CPU baseline
-def cpu_baseline(steps):
+def cpu_baseline(wl, steps):
     """The same train step on host cores for a bounded sample (1 sample/step)."""
-    from oracle.cpu_path import cpu_ops, depth_images
-    from svdformer_pointsea_amd.render import PCViews
-    from svdformer_pointsea_amd.svdformer import Model, PCNConfig, get_loss
+    from oracle.cpu_path import cpu_ops
 
     nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(nthreads)
     torch.manual_seed(0)
-    model = Model(PCNConfig)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999))
-    render = PCViews(TRANS=-PCNConfig.NETWORK.view_distance, RESOLUTION=224)
-    partial, gt = synth_pcn(1, 12345, "cpu")
+    model = wl.Model(wl.cfg)
+    opt = wl.optimizer(model.parameters())
+    partial, gt = wl.synth(1, 12345, "cpu")
 
     def step():
-        depth = depth_images(render, partial).unsqueeze(1)
-        loss, _ = get_loss(model(partial, depth), gt)
+        depth = wl.images(partial, cpu=True)
+        loss = wl.loss(model(partial, depth), partial, gt)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
@@ -208,8 +289,9 @@ def cpu_baseline(steps):
             step()
         dt = time.perf_counter() - t0
     return {"value": steps / dt, "unit": "samples/s", "cores": nthreads, "kind": "port",
-            "sample": f"{steps} train steps of 1 PCN sample (2048->16384) after 1 warm-up, fp32: torch CPU "
-                      f"({nthreads} threads) + oracle/pcops_oracle.c point ops (1 thread) + torch CPU attention"}
+            "sample": f"{steps} train steps of 1 {wl.name} sample (2048->{wl.n_out}) after 1 warm-up, fp32: "
+                      f"torch CPU ({nthreads} threads) + oracle/pcops_oracle.c point ops (1 thread) + torch CPU "
+                      f"attention"}
 
 
 # ------------------------------------------------------------------ main
@@ -229,28 +311,31 @@ def main():
 
     import svdformer_pointsea_amd as pkg
     from svdformer_pointsea_amd import _lib
-    from svdformer_pointsea_amd.render import PCViews
-    from svdformer_pointsea_amd.svdformer import Model, PCNConfig, get_loss
 
     pkg.lib()  # fail loudly if libpcops.so is missing
+    wl = Workload(args.model)
+    if args.batch is None:
+        args.batch = wl.batch
     torch.manual_seed(0)  # identical init on every rank
-    model = Model(PCNConfig).to(device)
+    model = wl.Model(wl.cfg).to(device)
     nparams = sum(p.numel() for p in model.parameters())
     bucket = GradBucket(model.parameters(), device)
     use_graph = not args.no_graph
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, betas=(0.9, 0.999), weight_decay=0, fused=True,
-                           capturable=use_graph)
-    render = PCViews(TRANS=-PCNConfig.NETWORK.view_distance, RESOLUTION=224)
-    partial, gt = synth_pcn(args.batch, 1000 + rank, device)
+    opt = wl.optimizer(model.parameters(), fused=True, capturable=use_graph)
+    partial, gt = wl.synth(args.batch, 1000 + rank, device)
+    # ShapeNet-55 re-crops its partial input from gt inside the step; the crop
+    # draws come from the device's default generator (graph-capturable)
+    crop_rng = torch.cuda.default_generators[device.index] if args.model == "pointsea" else None
     loss_acc = torch.zeros((), device=device)
     amp = not args.fp32
 
     def fwd_bwd():
         bucket.zero()
-        depth = render.get_img(partial).unsqueeze(1)
+        inp = wl.inputs(partial, gt, crop_rng)
+        depth = wl.images(inp)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=not use_graph):
-            pcds = model(partial, depth)
-            loss, _ = get_loss(pcds, gt)
+            pcds = model(inp, depth)
+            loss = wl.loss(pcds, inp, gt)
         loss.backward()
         loss_acc.add_(loss.detach())  # logged without a host sync
 
@@ -326,7 +411,7 @@ def main():
     if rank == 0:
         samples = args.batch * world * args.steps
         out = {
-            "metric": "train-step samples/sec (PCN, B=32, 2048->16384 pts)",
+            "metric": wl.metric,
             "value": samples / elapsed,
             "unit": "samples/s",
             "n_gpus": world,
@@ -341,10 +426,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.fp32 else "bf16",
-            "data": "synthetic (random ellipsoid-surface PCN-shaped clouds, random-init weights)",
-            "config": {"workload": "SVDFormer PCN train step: render + fwd + get_loss + bwd + Adam",
+            "data": f"synthetic (random ellipsoid-surface {args.model} clouds, random-init weights)",
+            "config": {"workload": wl.desc,
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch, "points_in": 2048,
-                       "points_out": 16384, "params": nparams,
+                       "points_out": wl.n_out, "params": nparams,
                        "parallelism": f"dp{world}" if world > 1 else "single"},
         }
         timed = {k: r for k, r in rows.items() if "frac" in r}
@@ -368,7 +453,7 @@ def main():
                                   **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {})}
                               for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_steps)
+            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -133,12 +133,27 @@ def depth_images(render, points):
                                            render.resolution, render.resolution))
 
 
+def real_images(render, points):
+    """PCViews_Real.get_img on CPU -> (B*V, 3, 224, 224): the view transform in
+    torch (mv_utils_zs.py:166-195), then the oracle's points2grid / grid2image."""
+    b = points.shape[0]
+    v = render.num_views
+    p = torch.repeat_interleave(points.detach().float(), v, dim=0)
+    p = torch.matmul(p, render.rot_mat.repeat(b, 1, 1))
+    p = torch.matmul(p, render.rot_mat2.repeat(b, 1, 1))
+    p = p - render.translation.unsqueeze(1).repeat(b, 1, 1)
+    grid = O.points2grid(_np(p))
+    return torch.from_numpy(O.grid2image(grid, render.kernel.numpy()))
+
+
 @contextlib.contextmanager
 def cpu_ops():
     """Swap the package's HIP entry points for the CPU versions above."""
-    from svdformer_pointsea_amd import attention, chamfer3D, model_utils, pointnet2_utils, svdformer
+    from svdformer_pointsea_amd import attention, chamfer3D, model_utils, pointnet2_utils, pointsea, svdformer
 
     patches = [
+        (pointsea, "furthest_point_sample", _FPS.apply),
+        (pointsea, "gather_operation", _Gather.apply),
         (pointnet2_utils, "furthest_point_sample", _FPS.apply),
         (pointnet2_utils, "gather_operation", _Gather.apply),
         (pointnet2_utils, "grouping_operation", _Group.apply),

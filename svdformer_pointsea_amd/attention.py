@@ -418,7 +418,12 @@ class SDG_Decoder_PointSea(nn.Module):
         self.sa1 = self_attention_woinp(hidden_dim, hidden_dim, dropout=dropout, nhead=8)
         self.sa2 = self_attention_woinp(hidden_dim, hidden_dim, dropout=dropout, nhead=8)
 
-    def forward(self, input, pos=None):
+    def forward_tokens(self, x_tok):
+        s, f = self.sa1.forward_tokens(x_tok)
+        s, f = self.sa2.forward_tokens(s + f)
+        return s + f
+
+    def forward(self, input, pos=None):  # pos is accepted and unused, as in the reference
         s, f = self.sa1.forward_tokens(to_tokens(input))
         s, f = self.sa2.forward_tokens(s + f)
         return to_channels(s, f, s.dtype)

@@ -1,0 +1,84 @@
+"""On-device data preparation of the ShapeNet-55 train loop.
+
+seprate_point_cloud   utils/helpers.py:62-123 (online cropping: the points
+                      nearest a random unit-sphere centre are cut away, the
+                      rest is FPS-subsampled to 2048), called inside the
+                      step by core/train_55.py:150.
+
+The reference loops over the batch and issues two FPS launches per sample
+on ragged clouds (N - num_crop and num_crop points).  Here the whole batch
+goes through two batched FPS launches: every sample's kept (or cropped)
+points are packed to the front of a (B, N_max, 3) buffer and the tail is
+zero-filled.  That is exact, not an approximation: the FPS kernel never
+selects a point with |p|^2 <= 1e-3 and never lets one update the running
+distances (sampling_gpu.cu:100-101), the surviving points keep their
+indices, and the block size (hence the tie rule) is 512 for every N >= 512,
+so the selected indices are those of the per-sample ragged call.
+"""
+import random
+
+import torch
+import torch.nn.functional as F
+
+from .model_utils import fps_subsample
+
+
+def _pack(points, order, start, count, n_max):
+    """rows order[b, start[b] : start[b] + count[b]] of points[b], packed to the
+    front of a (B, n_max, 3) buffer with a zero tail."""
+    B, N, _ = points.shape
+    j = torch.arange(n_max, device=points.device).unsqueeze(0)
+    src = (start.unsqueeze(1) + j).clamp_(max=N - 1)
+    keep = j < count.unsqueeze(1)
+    idx = torch.gather(order, 1, src)
+    out = torch.gather(points, 1, idx.unsqueeze(-1).expand(B, n_max, 3))
+    return out * keep.unsqueeze(-1).to(out.dtype)
+
+
+def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=False, generator=None):
+    """utils/helpers.py:62-123 -> (input_data, crop_data).
+
+    crop: int, or [lo, hi] for a per-sample random crop size (then both parts
+    are FPS-subsampled to 2048, as the reference does).  fixed_points: None
+    (random unit centre per sample), one (3,) point or a list to sample from.
+    `generator` (optional, a torch.Generator on xyz's device) replaces the
+    reference's global `random` / `torch.randn` draws for reproducible runs."""
+    B, n, c = xyz.shape
+    assert n == num_points
+    assert c == 3
+    if crop == num_points:
+        return xyz, None
+    dev = xyz.device
+    if isinstance(crop, list):
+        if generator is None:
+            num_crop = torch.tensor([random.randint(crop[0], crop[1]) for _ in range(B)], device=dev)
+        else:
+            num_crop = torch.randint(crop[0], crop[1] + 1, (B,), device=dev, generator=generator)
+    else:
+        num_crop = torch.full((B,), int(crop), device=dev)
+    if fixed_points is None:
+        if generator is None:
+            center = F.normalize(torch.randn(B, 1, 3), p=2, dim=-1).to(dev)
+        else:
+            center = F.normalize(torch.randn(B, 1, 3, device=dev, generator=generator), p=2, dim=-1)
+    else:
+        pts = fixed_points if isinstance(fixed_points, list) else [fixed_points]
+        center = torch.stack([torch.as_tensor(random.sample(pts, 1)[0], dtype=xyz.dtype).reshape(1, 3)
+                              for _ in range(B)]).to(dev)
+    dist = torch.norm(center - xyz, p=2, dim=-1)           # (B, n)
+    order = torch.argsort(dist, dim=-1, descending=False)
+    if padding_zeros:
+        keep = torch.arange(n, device=dev).unsqueeze(0) >= num_crop.unsqueeze(1)
+        mask = torch.zeros(B, n, dtype=torch.bool, device=dev).scatter_(1, order, keep)
+        input_data = xyz * mask.unsqueeze(-1).to(xyz.dtype)
+    if isinstance(crop, list):
+        hi = int(crop[1])
+        if not padding_zeros:
+            input_data = _pack(xyz, order, num_crop, n - num_crop, n - int(crop[0]))
+        crop_data = _pack(xyz, order, torch.zeros_like(num_crop), num_crop, hi)
+        return fps_subsample(input_data.contiguous(), 2048), fps_subsample(crop_data.contiguous(), 2048)
+    k = int(crop)
+    if not padding_zeros:
+        input_data = torch.gather(xyz, 1, order[:, k:].unsqueeze(-1).expand(B, n - k, 3))
+    crop_data = torch.gather(xyz, 1, order[:, :k].unsqueeze(-1).expand(B, k, 3))
+    return input_data.contiguous(), crop_data.contiguous()
