@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="issue every launch from Python (no HIP graph)")
     ap.add_argument("--timing-steps", type=int, default=2, help="eager steps timed per launch (graph mode)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1_bench_graph_pmc_traffic.json"),
+                    help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
+                         "(tools/pmc_traffic.py) -> roofline.traffic")
     return ap.parse_args()
 
 
@@ -183,6 +186,28 @@ def kernel_work(name, a):
     return None
 
 
+# libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
+_SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
+            "attention bwd dkv": "attn_dkv2_kernel", "furthest_point_sampling": "fps_reg_kernel",
+            "chamfer_3D.forward": "chamfer_nn_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
+            "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel"}
+
+
+def pmc_traffic(path, key, name):
+    """Launch-weighted HBM bytes per launch of the kernels behind one call group,
+    from a tools/pmc_traffic.py summary (None if absent)."""
+    import re
+    if not path or not os.path.exists(path) or name not in _SYMBOLS:
+        return None
+    pat = _SYMBOLS[name]
+    m = re.search(r"D=(\d+)", key)
+    if m:  # attention kernels are instantiated per head dim: <D, ...> / ILiDE
+        pat += r"(<|ILi)%s(,|E)" % m.group(1)
+    rows = [v for k, v in json.load(open(path)).items() if re.search(pat, k)]
+    n = sum(r["launches"] for r in rows)
+    return sum(r["hbm_bytes_per_launch"] * r["launches"] for r in rows) / n if n else None
+
+
 def kernel_table(spans):
     """Group recorded calls by (name, shape) and attach roofline fractions."""
     rows = {}
@@ -256,11 +281,16 @@ class Workload:
         n = gt.shape[1]
         return seprate_point_cloud(gt, n, [n // 4, 3 * n // 4], generator=generator)[0]
 
-    def loss(self, pcds, partial, gt):
+    def gt_pyramid(self, gt):
+        """The loss's gt FPS chain (n_out -> 2048 -> 256); depends on gt only."""
+        from svdformer_pointsea_amd.metrics import gt_pyramid
+        return gt_pyramid(gt, 2048, 256)
+
+    def loss(self, pcds, partial, gt, gts=None):
         from svdformer_pointsea_amd.metrics import get_loss, get_loss_PM
         if self.name == "svdformer":
-            return get_loss(pcds, gt, sqrt=True)[0]
-        return get_loss_PM(pcds, partial, gt, sqrt=False)[0]
+            return get_loss(pcds, gt, sqrt=True, gts=gts)[0]
+        return get_loss_PM(pcds, partial, gt, sqrt=False, gts=gts)[0]
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -331,11 +361,15 @@ def main():
 
     def fwd_bwd():
         bucket.zero()
+        # the loss's gt FPS chain depends on gt only: it runs on a second
+        # stream beside the whole forward pass (FPS occupies B CUs)
+        with _lib.fork(device, lane=1) as br:
+            gts = wl.gt_pyramid(gt)
         inp = wl.inputs(partial, gt, crop_rng)
         depth = wl.images(inp)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=not use_graph):
             pcds = model(inp, depth)
-            loss = wl.loss(pcds, inp, gt)
+            loss = wl.loss(pcds, inp, gt, br.join(*gts))
         loss.backward()
         loss_acc.add_(loss.detach())  # logged without a host sync
 
@@ -438,7 +472,9 @@ def main():
             d = timed[dom_key]
             out["roofline"] = {"kernel": dom_key, "bound": d["bound"], "achieved": round(d["achieved"], 2),
                                "peak": d["peak"] / (1e12 if d["unit"] == "TFLOP/s" else 1e9), "unit": d["unit"],
-                               "frac": round(d["frac"], 4), "traffic": None,
+                               "frac": round(d["frac"], 4),
+                               "traffic": pmc_traffic(args.pmc_json, dom_key, d["name"]),
+                               "traffic_source": os.path.relpath(args.pmc_json, ROOT) if args.pmc_json else None,
                                "avg_launch_ms": round(d["ms"] / d["launches"], 4),
                                "work_per_launch": d["work"] / d["launches"]}
             group = [r for r in timed.values() if r["name"] in ("furthest_point_sampling", "knn",

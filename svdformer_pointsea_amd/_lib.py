@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libpcops.so")
+# PCOPS_LIB_PATH selects an alternative build of the same C-ABI (A/B kernel experiments)
+LIB_PATH = os.environ.get("PCOPS_LIB_PATH") or os.path.join(_HERE, "_lib", "libpcops.so")
 
 _lib = None
 
@@ -160,6 +161,50 @@ def require_int(t, name):
     require_gpu(t, name)
     if t.dtype != torch.int32:
         raise RuntimeError(f"{name} must be an int tensor")
+
+
+_SIDE = {}
+
+
+def side_stream(device, lane=0):
+    """Extra HIP streams per device (lane 0, 1, ...) for independent work that
+    can run beside the current stream (the point ops fill only B of 256 CUs)."""
+    key = (torch.device(device).index, lane)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
+class fork:
+    """`with fork(device) as s:` runs the block on the side stream after the
+    current stream's pending work; `join(*tensors)` makes the current stream
+    wait for it and marks the tensors as used there.  No-op on CPU tensors."""
+
+    def __init__(self, device, lane=0):
+        self.on = torch.device(device).type == "cuda"
+        if self.on:
+            self.main = torch.cuda.current_stream(device)
+            self.side = side_stream(device, lane)
+
+    def __enter__(self):
+        if self.on:
+            self.side.wait_stream(self.main)
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self._ctx.__exit__(*exc)
+        return False
+
+    def join(self, *tensors):
+        if self.on:
+            self.main.wait_stream(self.side)
+            for t in tensors:
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(self.main)
+        return tensors[0] if len(tensors) == 1 else tensors
 
 
 class Workspace:

@@ -383,20 +383,56 @@ __device__ __forceinline__ float swap_halves_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// acc += Rows(32 x D, LDS row stride RS) . Ent   (entity fragment f)
-template <int D, int RS>
+// LDS tile image of the v2 kernels: rows of RS bf16 whose 16-B chunks are
+// XOR-permuted per row (chunk ch of row r sits at chunk ch ^ f(r)), so that
+// BOTH reads of a tile are bank-conflict free on gfx950: the row reads of
+// k_product (ds_read_b128, 4 x 16-lane groups) and the transposed reads of
+// v_product (ds_read_b64_tr_b16, 2 x 32-lane groups).  f depends on row bits
+// 0..3 only, so a tile's second 32-row half uses the same f.  The maps were
+// found and are checked by tools/lds_banks.py (a plain D+8 pad made the
+// transposed reads 2-4 way conflicted: 14 % of dK/dV wave cycles).
+template <int D>
+struct Img;
+template <>
+struct Img<32> {
+  static constexpr int RS = 40;
+  __device__ static constexpr int f(int) { return 0; }
+};
+template <>
+struct Img<64> {
+  static constexpr int RS = 64;
+  __device__ static constexpr int f(int r) { return ((r & 3) << 1) ^ ((r >> 2) & 3); }
+};
+template <>
+struct Img<96> {
+  static constexpr int RS = 96;
+  __device__ static constexpr int f(int r) { return (r & 1) ^ ((r >> 2) & 3); }
+};
+template <>
+struct Img<128> {
+  static constexpr int RS = 128;
+  __device__ static constexpr int f(int r) { return ((r & 3) << 2) ^ ((r >> 2) & 3); }
+};
+
+// element (row, 8*ch + e) of an Img<D> tile
+template <int D>
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return row * Img<D>::RS + 8 * (ch ^ Img<D>::f(row));
+}
+
+// acc += Rows(32 x D, Img<D> tile) . Ent   (entity fragment f)
+template <int D>
 __device__ __forceinline__ void k_product(f32x16 &acc, const __bf16 *lds, const bf16x8 (&f)[D / 16]) {
-  const int l = lane_(), h = l >> 5;
-  const __bf16 *rp = lds + (l & 31) * RS + 8 * h;
+  const int l = lane_(), h = l >> 5, row = l & 31;
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8 *>(rp + 16 * s);
+    const bf16x8 a = *reinterpret_cast<const bf16x8 *>(lds + img_off<D>(row, 2 * s + h));
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, f[s], acc, 0, 0, 0);
   }
 }
 
-// Y[db] += Rows^T(D x 32, LDS row stride RS) . X   (X = fp32 accumulator of 32 rows)
-template <int D, int RS>
+// Y[db] += Rows^T(D x 32, Img<D> tile) . X   (X = fp32 accumulator of 32 rows)
+template <int D>
 __device__ __forceinline__ void v_product(f32x16 (&Y)[D / 32], const __bf16 *lds, const f32x16 &X) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
@@ -409,9 +445,9 @@ __device__ __forceinline__ void v_product(f32x16 (&Y)[D / 32], const __bf16 *lds
     const int row0 = 16 * s + 4 * h + q;
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
-      const int col = db * 32 + 16 * g + 4 * p;
-      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + row0 * RS + col));
-      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + (row0 + 8) * RS + col));
+      const int ch = 4 * db + 2 * g + (p >> 1), e = 4 * (p & 1);
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0, ch) + e));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0 + 8, ch) + e));
       const bf16x8 a = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1,
                                                2, 3, 4, 5, 6, 7);
       Y[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, Y[db], 0, 0, 0);
@@ -432,11 +468,19 @@ __device__ __forceinline__ void xcd_block(int &rb, int &bh) {
   bh = L / nrb;
 }
 
+// Occupancy of the backward passes.  dQ (template OCC): 2 waves per SIMD for
+// D <= 96 (D=96 0.093 -> 0.060 ms at the PCN shapes), 1 for D = 128 (its
+// 256-register form spills).  dK/dV stays at one (forcing two spills its
+// dK/dV accumulators: D=128 2.4 -> 4.3 ms); PCOPS_DKV_OCC is for A/B builds.
+#ifndef PCOPS_DKV_OCC
+#define PCOPS_DKV_OCC
+#endif
+
 template <int D, int NW>
 struct Fwd2Cfg {
   static constexpr int kThr = NW * 64;
-  static constexpr int kKS = D + 8;                 // K tile row stride (b128 row reads)
-  static constexpr int kVS = D + 8;                 // V tile row stride (tr reads)
+  static constexpr int kKS = Img<D>::RS;            // tile row stride (both tiles: Img<D>)
+  static constexpr int kVS = Img<D>::RS;
   static constexpr int kChunks = kKT * D / 8;       // 16-B chunks per tile
   static constexpr int kCPT = (kChunks + kThr - 1) / kThr;
   static constexpr int kKBuf = kKT * kKS, kVBuf = kKT * kVS;
@@ -468,8 +512,8 @@ __device__ __forceinline__ void fwd2_store(__bf16 *sk, __bf16 *sv, const typenam
     const int c = threadIdx.x + t * C::kThr;
     if (C::kChunks % C::kThr != 0 && c >= C::kChunks) continue;
     const int row = c / (D / 8), ch = c % (D / 8);
-    *reinterpret_cast<bf16x8 *>(sk + row * C::kKS + ch * 8) = kr[t];
-    *reinterpret_cast<bf16x8 *>(sv + row * C::kVS + ch * 8) = vr[t];
+    *reinterpret_cast<bf16x8 *>(sk + img_off<D>(row, ch)) = kr[t];
+    *reinterpret_cast<bf16x8 *>(sv + img_off<D>(row, ch)) = vr[t];
   }
 }
 
@@ -512,8 +556,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
     f32x16 X0 = f32x16{}, X1 = f32x16{};
-    k_product<D, C::kKS>(X0, ck, qf);
-    k_product<D, C::kKS>(X1, ck + 32 * C::kKS, qf);
+    k_product<D>(X0, ck, qf);
+    k_product<D>(X1, ck + 32 * C::kKS, qf);
     if (k0 + kKT > Lk) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -541,8 +585,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) Y[db] *= alpha;
     }
-    v_product<D, C::kVS>(Y, cv, X0);
-    v_product<D, C::kVS>(Y, cv + 32 * C::kVS, X1);
+    v_product<D>(Y, cv, X0);
+    v_product<D>(Y, cv + 32 * C::kVS, X1);
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   }
@@ -566,8 +610,8 @@ int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse
 
 // ----------------------------------------------------------------- backward, bf16 (v2)
 // dQ pass: queries on the lane, K/V 64-row tiles double-buffered (as forward).
-template <int D, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
+template <int D, int NW, int OCC>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dq2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
                                                            const __bf16 *__restrict__ V, const __bf16 *__restrict__ dO,
                                                            const float *__restrict__ lse,
                                                            const float *__restrict__ delta, __bf16 *__restrict__ dQ,
@@ -612,10 +656,10 @@ __global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restr
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
     f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
-    k_product<D, C::kKS>(S0, ck, qf);
-    k_product<D, C::kKS>(S1, ck + 32 * C::kKS, qf);
-    k_product<D, C::kVS>(G0, cv, gf);
-    k_product<D, C::kVS>(G1, cv + 32 * C::kVS, gf);
+    k_product<D>(S0, ck, qf);
+    k_product<D>(S1, ck + 32 * C::kKS, qf);
+    k_product<D>(G0, cv, gf);
+    k_product<D>(G1, cv + 32 * C::kVS, gf);
     const bool edge = k0 + kKT > Lk;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -628,8 +672,8 @@ __global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restr
       S0[r] = p0 * (G0[r] - dl);  // dS^T without the softmax scale
       S1[r] = p1 * (G1[r] - dl);
     }
-    v_product<D, C::kKS>(Y, ck, S0);
-    v_product<D, C::kKS>(Y, ck + 32 * C::kKS, S1);
+    v_product<D>(Y, ck, S0);
+    v_product<D>(Y, ck + 32 * C::kKS, S1);
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   }
@@ -638,7 +682,7 @@ __global__ __launch_bounds__(NW * 64) void attn_dq2_kernel(const __bf16 *__restr
 
 // dK/dV pass: keys on the lane, Q/dO 64-row tiles (+ their lse/delta) double-buffered.
 template <int D, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_dkv2_kernel(const __bf16 *__restrict__ Q,
+__global__ __launch_bounds__(NW * 64) PCOPS_DKV_OCC void attn_dkv2_kernel(const __bf16 *__restrict__ Q,
                                                             const __bf16 *__restrict__ K,
                                                             const __bf16 *__restrict__ V,
                                                             const __bf16 *__restrict__ dO,
@@ -709,10 +753,10 @@ __global__ __launch_bounds__(NW * 64) void attn_dkv2_kernel(const __bf16 *__rest
     const float *cl = slse + cur * kKT;
     const float *cd = sdl + cur * kKT;
     f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
-    k_product<D, C::kKS>(S0, cq, kf);                 // S  (queries x keys)
-    k_product<D, C::kKS>(S1, cq + 32 * C::kKS, kf);
-    k_product<D, C::kVS>(G0, cg, vf);                 // dP (queries x keys)
-    k_product<D, C::kVS>(G1, cg + 32 * C::kVS, vf);
+    k_product<D>(S0, cq, kf);                 // S  (queries x keys)
+    k_product<D>(S1, cq + 32 * C::kKS, kf);
+    k_product<D>(G0, cg, vf);                 // dP (queries x keys)
+    k_product<D>(G1, cg + 32 * C::kVS, vf);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = acc_row(r, h);
@@ -723,10 +767,10 @@ __global__ __launch_bounds__(NW * 64) void attn_dkv2_kernel(const __bf16 *__rest
       G0[r] = p0 * (G0[r] - cd[row]);
       G1[r] = p1 * (G1[r] - cd[row + 32]);
     }
-    v_product<D, C::kVS>(Y1, cg, S0);  // dV^T += dO^T P
-    v_product<D, C::kVS>(Y1, cg + 32 * C::kVS, S1);
-    v_product<D, C::kKS>(Y2, cq, G0);  // dK^T += Q^T dS
-    v_product<D, C::kKS>(Y2, cq + 32 * C::kKS, G1);
+    v_product<D>(Y1, cg, S0);  // dV^T += dO^T P
+    v_product<D>(Y1, cg + 32 * C::kVS, S1);
+    v_product<D>(Y2, cq, G0);  // dK^T += Q^T dS
+    v_product<D>(Y2, cq + 32 * C::kKS, G1);
     if (t + 1 < ntiles) {
       fwd2_store<D, NW>(sq + (cur ^ 1) * C::kKBuf, sg + (cur ^ 1) * C::kVBuf, qr, gr);
       if (threadIdx.x < kKT) {
@@ -744,11 +788,12 @@ template <int D, int NW>
 int launch_dq2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                void *dq, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW>,
+  constexpr int OCC = D <= 96 ? 2 : 1;
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_dq2_kernel<D, NW>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
                      (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dq, Lq, Lk,
                      scale, st);
   PC_CHECK_LAUNCH();

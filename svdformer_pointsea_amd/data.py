@@ -20,6 +20,7 @@ import random
 import torch
 import torch.nn.functional as F
 
+from ._lib import fork
 from .model_utils import fps_subsample
 
 
@@ -76,7 +77,11 @@ def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=
         if not padding_zeros:
             input_data = _pack(xyz, order, num_crop, n - num_crop, n - int(crop[0]))
         crop_data = _pack(xyz, order, torch.zeros_like(num_crop), num_crop, hi)
-        return fps_subsample(input_data.contiguous(), 2048), fps_subsample(crop_data.contiguous(), 2048)
+        # the two FPS launches (B workgroups each) run side by side
+        with fork(dev) as br:
+            crop_out = fps_subsample(crop_data.contiguous(), 2048)
+        input_out = fps_subsample(input_data.contiguous(), 2048)
+        return input_out, br.join(crop_out)
     k = int(crop)
     if not padding_zeros:
         input_data = torch.gather(xyz, 1, order[:, k:].unsqueeze(-1).expand(B, n - k, 3))

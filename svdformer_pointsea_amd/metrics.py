@@ -44,23 +44,31 @@ def chamfer_single_side_sqrt(pcd1, pcd2):
     return _means(pcd1, pcd2, True)[0]
 
 
-def _stage_losses(pcds_pred, gt, CD):
+def gt_pyramid(gt, n1, nc):
+    """(gt_c, gt_1): gt FPS-subsampled to n1 points, then that to nc points
+    (loss_utils.py:47-48).  It depends on gt only, so a caller may compute it
+    ahead of (and beside) the forward pass and hand it to get_loss(gts=...)."""
+    gt_1 = fps_subsample(gt, n1)
+    return fps_subsample(gt_1, nc), gt_1
+
+
+def _stage_losses(pcds_pred, gt, CD, gts=None):
     """CD of (coarse, fine1, fine2) against gt FPS-subsampled to each size."""
     Pc, P1, P2 = pcds_pred
-    gt_1 = fps_subsample(gt, P1.shape[1])
-    gt_c = fps_subsample(gt_1, Pc.shape[1])
+    gt_c, gt_1 = gts if gts is not None else gt_pyramid(gt, P1.shape[1], Pc.shape[1])
     return [CD(Pc, gt_c), CD(P1, gt_1), CD(P2, gt)]
 
 
-def get_loss(pcds_pred, gt, sqrt=True, alpha1=1, alpha2=1):
-    """loss_utils.py:33-58 -> (cdc + alpha1*cd1 + alpha2*cd2, [cdc, cd1, cd2])."""
-    cdc, cd1, cd2 = _stage_losses(pcds_pred, gt, chamfer_sqrt if sqrt else chamfer)
+def get_loss(pcds_pred, gt, sqrt=True, alpha1=1, alpha2=1, gts=None):
+    """loss_utils.py:33-58 -> (cdc + alpha1*cd1 + alpha2*cd2, [cdc, cd1, cd2]).
+    `gts` (optional): gt_pyramid(gt, ...) computed earlier by the caller."""
+    cdc, cd1, cd2 = _stage_losses(pcds_pred, gt, chamfer_sqrt if sqrt else chamfer, gts)
     return cdc + alpha1 * cd1 + alpha2 * cd2, [cdc, cd1, cd2]
 
 
-def get_loss_PM(pcds_pred, partial, gt, sqrt=True):
+def get_loss_PM(pcds_pred, partial, gt, sqrt=True, gts=None):
     """loss_utils.py:60-82: get_loss + single-sided partial -> fine2 matching."""
-    cdc, cd1, cd2 = _stage_losses(pcds_pred, gt, chamfer_sqrt if sqrt else chamfer)
+    cdc, cd1, cd2 = _stage_losses(pcds_pred, gt, chamfer_sqrt if sqrt else chamfer, gts)
     pm = (chamfer_single_side_sqrt if sqrt else chamfer_single_side)(partial, pcds_pred[2])
     return cdc + cd1 + cd2 + pm, [cdc, cd1, cd2]
 

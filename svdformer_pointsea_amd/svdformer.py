@@ -22,6 +22,7 @@ from torch import nn
 from .attention import SDG_Decoder, cross_attention, self_attention, to_channels, to_tokens
 from .chamfer3D import chamfer_3DDist
 from .model_utils import fps_subsample, group_local, sample_and_group_knn
+from ._lib import fork
 from .pointnet2_utils import furthest_point_sample, gather_operation
 
 
@@ -427,8 +428,12 @@ class Model(nn.Module):
 
     def forward(self, partial, depth):
         partial_cm = partial.transpose(1, 2).contiguous()
+        # the local encoder (EdgeConv kNN, FPS) only depends on the partial cloud:
+        # it runs on a second HIP stream beside the view/point encoder
+        with fork(partial.device) as br:
+            local_feat = self.localencoder(partial_cm)
         feat_g, coarse = self.encoder(partial_cm, depth)
-        local_feat = self.localencoder(partial_cm)
+        local_feat = br.join(local_feat)
         coarse_merge = torch.cat([partial_cm, coarse.to(partial_cm.dtype)], dim=2).float().contiguous()
         coarse_merge = gather_operation(coarse_merge, furthest_point_sample(coarse_merge.transpose(1, 2).contiguous(),
                                                                             self.merge_points))

@@ -12,8 +12,11 @@ B = 32
 shapes = [  # (Lq, Lk, E, H) seen in the PCN step
     (2048, 2048, 512, 8), (2048, 2048, 1024, 8), (2048, 512, 512, 8), (512, 512, 768, 8), (512, 512, 512, 8),
     (128, 128, 512, 4)]
-tag = "v1" if os.environ.get("PCOPS_ATTN_V1") == "1" else "v2"
-for Lq, Lk, E, H in shapes:
+tag = os.environ.get("PCOPS_LIB_PATH", "v1" if os.environ.get("PCOPS_ATTN_V1") == "1" else "v2")
+sel = [int(a) for a in sys.argv[1:]]
+for si, (Lq, Lk, E, H) in enumerate(shapes):
+    if sel and si not in sel:
+        continue
     q = torch.randn(Lq, B, E, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(Lk, B, E, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(Lk, B, E, device="cuda", dtype=torch.bfloat16, requires_grad=True)

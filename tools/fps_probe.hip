@@ -6,8 +6,8 @@
 #include <vector>
 
 int main() {
-  for (int N : {2048, 16384}) {
-    const int B = 32, M = N / 8;
+  for (int N : {2048, 6144, 8192, 16384}) {
+    const int B = 32, M = N >= 6144 ? 2048 : N / 4;
     std::vector<float> h(B * N * 3);
     unsigned s = 12345;
     for (auto &v : h) { s = s * 1664525u + 1013904223u; v = (s >> 8) * (1.0f / 16777216.0f) - 0.5f; }
