@@ -20,6 +20,8 @@ def fill_state(module, seed, scale=0.05):
         shape = tuple(t.shape)
         if key.endswith("norm12.weight") or key.endswith("norm13.weight"):
             v = 1.0 + 0.1 * rng.standard_normal(shape)
+        elif key.endswith("running_var"):  # BatchNorm eval statistics must stay positive
+            v = 1.0 + 0.1 * np.abs(rng.standard_normal(shape))
         else:
             v = scale * rng.standard_normal(shape)
         new[key] = torch.from_numpy(v.astype(np.float32))

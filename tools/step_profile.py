@@ -77,3 +77,10 @@ for g, t in sorted(groups.items(), key=lambda kv: -kv[1]):
 print()
 for n, (c, t) in sorted(kern.items(), key=lambda kv: -kv[1][1])[:args.rows]:
     print(f"{t / 1e3:8.3f} ms {c:5d}x  {n[:150]}")
+
+if os.environ.get("SHAPES"):
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof2:
+        step()
+        torch.cuda.synchronize()
+    print(prof2.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=args.rows,
+                                                               max_name_column_width=30, max_shapes_column_width=100))
