@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="issue every launch from Python (no HIP graph)")
     ap.add_argument("--timing-steps", type=int, default=2, help="eager steps timed per launch (graph mode)")
+    ap.add_argument("--tunableop", choices=("use", "tune", "off"), default="use",
+                    help="PyTorch TunableOp for the dense GEMMs: 'use' the committed per-shape hipBLASLt "
+                         "selections in tuning/ (if present), 'tune' them during warm-up (rank 0 "
+                         "writes the file), or 'off' (library heuristics)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1_bench_graph_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
@@ -324,6 +328,42 @@ def cpu_baseline(wl, steps):
                       f"attention"}
 
 
+# ------------------------------------------------------------------ GEMM selection
+def setup_tunableop(mode, model, rank):
+    """hipBLASLt's default heuristic picks non-split-K tiles for the long-K
+    weight-gradient GEMMs of this model ((512..3072) x 65536 x (512..1024)),
+    leaving most of the 256 CUs idle.  PyTorch TunableOp times every hipBLASLt /
+    rocBLAS solution per GEMM shape once; the winners are kept in a CSV that is
+    committed and re-read on every run.  Returns the CSV path or None."""
+    if mode == "off":
+        return None
+    import torch.cuda.tunable as tunable
+    path = os.path.join(ROOT, "tuning", f"tunableop_{model}_gfx950.csv")
+    if mode == "use" and not os.path.exists(path):
+        return None
+    tunable.enable(True)
+    tunable.tuning_enable(mode == "tune")
+    if mode == "tune":
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tunable.set_max_tuning_duration(5)     # ms per candidate solution
+        tunable.set_max_tuning_iterations(8)
+        import threading
+
+        t0 = time.time()
+
+        def beat():  # tuning is silent for minutes; keep the job's output alive
+            while True:
+                time.sleep(20)
+                print(f"[tunableop] tuning, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+        threading.Thread(target=beat, daemon=True).start()
+        tunable.set_filename(path if rank == 0 else path + f".rank{rank}", False)
+    else:
+        tunable.set_filename(path + ".unused", False)  # never write next to the committed file
+        tunable.read_file(path)
+    return path
+
+
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -343,6 +383,7 @@ def main():
     from svdformer_pointsea_amd import _lib
 
     pkg.lib()  # fail loudly if libpcops.so is missing
+    tuned = setup_tunableop(args.tunableop, args.model, rank)
     wl = Workload(args.model)
     if args.batch is None:
         args.batch = wl.batch
@@ -454,6 +495,8 @@ def main():
             "ms_per_step": elapsed * 1e3 / args.steps,
             "host_issue_ms_per_step": host * 1e3 / args.steps,
             "execution": "hip_graph" if use_graph else "eager",
+            "gemm_selection": (f"TunableOp ({args.tunableop}): {os.path.relpath(tuned, ROOT)}" if tuned
+                               else "hipBLASLt heuristics"),
             "kernel_timing": ("HIP events per libpcops launch, %d eager steps after the timed graph replays"
                               % args.timing_steps) if use_graph else "HIP events per libpcops launch, timed steps",
             "higher_is_better": True,

@@ -10,6 +10,8 @@
 //   dot  = sequential fma chain over channels (sgemm micro-kernel)
 //   |v|^2 = torch.sum(v**2,-1) reduction order (see torch_sumsq below)
 //   d = ((-2*dot) + |q|^2) + |p|^2
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -250,6 +252,112 @@ __global__ __launch_bounds__(64 * G) void knnC_kernel(const float *__restrict__ 
                          dist ? dist + ((size_t)b * S + sc) * K : nullptr);
 }
 
+
+// generic C, v2 (C >= 32): distance tiles on a 4x4 register micro-tile.
+// Block = 64 queries; candidates in tiles of 64, channels staged 32 at a time
+// for both sides ([64][36] float images: the 16 lanes of a ds_read_b128 group
+// read 16 consecutive rows -> conflict-free).  Thread (tq, tc) accumulates the
+// dots of queries tq+16i x candidates tc+16j over the channels IN ORDER (the
+// sequential fma chain of the oracle / torch CPU sgemm), so the distance bits
+// equal knnC_kernel's.  The 64x64 distance tile goes to LDS, then thread
+// (w, lane) runs the top-KK insertion for query `lane` over candidates
+// [16w, 16w+16) of the tile -- the same 4-way split + (distance, index) merge
+// as knnC_kernel.  The old kernel re-read every query row from global memory
+// per candidate tile and issued one LDS read per 4 fma; this one issues one
+// per 8 fma from LDS images and keeps 16 independent fma chains per thread.
+template <int KK>
+__global__ __launch_bounds__(256) void knnC2_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
+                                                    int N, int C, int K, int pad, int *__restrict__ idx,
+                                                    float *__restrict__ dist) {
+  constexpr int QT = 64, CT = 64, CC = 32, LS = CC + 4;
+  __shared__ __attribute__((aligned(16))) float sq[QT * LS];
+  __shared__ __attribute__((aligned(16))) float sp[CT * LS];
+  __shared__ float sd[QT][CT + 1];
+  __shared__ float sqn[QT], spn[CT];
+  __shared__ MergeBuf<KK, 4> mb;
+  const int b = blockIdx.y, t = threadIdx.x, tq = t >> 4, tc = t & 15;
+  const int w = t >> 6, lane = t & 63;
+  const int q0 = blockIdx.x * QT;
+  const float *qb = q + (size_t)b * S * C;
+  const float *pb = p + (size_t)b * N * C;
+  const int s = q0 + lane;
+  const int sc = s < S ? s : S - 1;
+  if (t < QT) sqn[t] = torch_sumsq(qb + (size_t)sc * C, C);
+  float bd[KK];
+  int bi[KK];
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    bd[k] = INFINITY;
+    bi[k] = 0;
+  }
+  for (int t0 = 0; t0 < N; t0 += CT) {
+    if (t < CT) spn[t] = t0 + t < N ? torch_sumsq(pb + (size_t)(t0 + t) * C, C) : 0.f;
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    for (int c0 = 0; c0 < C; c0 += CC) {
+      const int cw = min(CC, C - c0);
+      for (int e = t; e < QT * CC; e += 256) {
+        const int r = e / CC, c = e % CC;
+        const int qi = q0 + r, pi = t0 + r;
+        sq[r * LS + c] = (qi < S && c < cw) ? qb[(size_t)qi * C + c0 + c] : 0.f;
+        sp[r * LS + c] = (pi < N && c < cw) ? pb[(size_t)pi * C + c0 + c] : 0.f;
+      }
+      __syncthreads();
+      int c = 0;
+      for (; c + 4 <= cw; c += 4) {
+        float4 qv[4], pv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qv[i] = *reinterpret_cast<const float4 *>(sq + (tq + 16 * i) * LS + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pv[j] = *reinterpret_cast<const float4 *>(sp + (tc + 16 * j) * LS + c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[i][j] = __builtin_fmaf(qv[i].x, pv[j].x, acc[i][j]);
+            acc[i][j] = __builtin_fmaf(qv[i].y, pv[j].y, acc[i][j]);
+            acc[i][j] = __builtin_fmaf(qv[i].z, pv[j].z, acc[i][j]);
+            acc[i][j] = __builtin_fmaf(qv[i].w, pv[j].w, acc[i][j]);
+          }
+      }
+      for (; c < cw; ++c) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_fmaf(sq[(tq + 16 * i) * LS + c], sp[(tc + 16 * j) * LS + c], acc[i][j]);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        sd[tq + 16 * i][tc + 16 * j] = ((-2.f * acc[i][j]) + sqn[tq + 16 * i]) + spn[tc + 16 * j];
+    __syncthreads();
+    const int e1 = min(CT, N - t0);
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int e = w * 16 + k;
+      if (e < e1) topk_insert<KK>(bd, bi, sd[lane][e], t0 + e);
+    }
+    __syncthreads();
+  }
+  merge_and_store<KK, 4>(mb, bd, bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
+                         dist ? dist + ((size_t)b * S + sc) * K : nullptr);
+}
+
+bool knn_v1() {  // PCOPS_KNN_V1=1: the first-generation feature-space kernel (A/B runs)
+  static const bool v = [] {
+    const char *e = getenv("PCOPS_KNN_V1");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 template <int KK>
 int launch_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
                hipStream_t st) {
@@ -257,7 +365,17 @@ int launch_knn(const float *q, const float *p, int B, int S, int N, int C, int K
   const dim3 grid((S + 63) / 64, B);
   if (C == 3) {
     hipLaunchKernelGGL((knn3_kernel<KK, G>), grid, dim3(64 * G), 0, st, q, p, S, N, K, pad, idx, dist);
-  } else {
+    PC_CHECK_LAUNCH();
+    return PCOPS_OK;
+  }
+  if constexpr (KK <= 32) {
+    if (C >= 32 && !knn_v1()) {
+      hipLaunchKernelGGL((knnC2_kernel<KK>), grid, dim3(256), 0, st, q, p, S, N, C, K, pad, idx, dist);
+      PC_CHECK_LAUNCH();
+      return PCOPS_OK;
+    }
+  }
+  {
     const size_t lds = sizeof(float) * (32 * (size_t)C + 32);
     hipLaunchKernelGGL((knnC_kernel<KK, G>), grid, dim3(64 * G), lds, st, q, p, S, N, C, K, pad, idx, dist);
   }

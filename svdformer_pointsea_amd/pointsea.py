@@ -117,7 +117,7 @@ class SDG(nn.Module):
         s, f = self.sa1.forward_tokens(Fx, pos)
         F_Q = s + f
         F_Q_ = self.decoder1.forward_tokens(F_Q)           # PointSea's decoder ignores pos
-        f_g_current = F_Q.amax(dim=1, keepdim=True)        # torch.max(F_Q, 2)[0]
+        f_g_current = F_Q.max(dim=1, keepdim=True)[0]      # torch.max(F_Q, 2)[0]
         # similarity alignment
         local = _lin(self.mlpp.mlp[0], local_tok)
         s, f = self.cross1.forward_tokens(F_Q, local)
@@ -176,7 +176,7 @@ class SVFNet(nn.Module):
         # f_p.repeat(3, 1, n): image r (= 3b + v) is paired with f_p[r % B], as in the reference
         f_v_ = self.viewattn1(torch.cat([f_v, f_p.repeat(3, 1, f_v.size(2)).to(f_v.dtype)], 1))
         C = f_v_.shape[1]
-        f_v_ = f_v_.view(B, 3, C, -1).amax(dim=3).transpose(1, 2)     # '(b v) c n -> b c v n', max n
+        f_v_ = f_v_.view(B, 3, C, -1).max(dim=3)[0].transpose(1, 2)   # '(b v) c n -> b c v n', max n
         f_v_ = self.viewattn2(torch.cat([f_v_, f_p.repeat(1, 1, f_v_.size(2)).to(f_v_.dtype)], dim=1),
                               view_feature_1.permute(2, 0, 1))
         f_v_ = F.adaptive_max_pool1d(f_v_, 1)
