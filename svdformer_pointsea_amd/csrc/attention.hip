@@ -470,11 +470,7 @@ __device__ __forceinline__ void xcd_block(int &rb, int &bh) {
 
 // Occupancy of the backward passes.  dQ (template OCC): 2 waves per SIMD for
 // D <= 96 (D=96 0.093 -> 0.060 ms at the PCN shapes), 1 for D = 128 (its
-// 256-register form spills).  dK/dV stays at one (forcing two spills its
-// dK/dV accumulators: D=128 2.4 -> 4.3 ms); PCOPS_DKV_OCC is for A/B builds.
-#ifndef PCOPS_DKV_OCC
-#define PCOPS_DKV_OCC
-#endif
+// 256-register form spills).  dK/dV: see attn_dkv2_kernel's MODE.
 
 template <int D, int NW>
 struct Fwd2Cfg {
@@ -681,8 +677,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
 }
 
 // dK/dV pass: keys on the lane, Q/dO 64-row tiles (+ their lse/delta) double-buffered.
-template <int D, int NW>
-__global__ __launch_bounds__(NW * 64) PCOPS_DKV_OCC void attn_dkv2_kernel(const __bf16 *__restrict__ Q,
+// MODE 0: dK and dV in one pass (one wave per SIMD: both D x 32 accumulators
+// live).  MODE 1: dV only, MODE 2: dK only -- half the accumulators, so OCC = 2
+// waves per SIMD fit; the split pays one extra S recompute (5 instead of 4
+// GEMM units per key) for the second wave's latency hiding.
+template <int D, int NW, int MODE, int OCC>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dkv2_kernel(const __bf16 *__restrict__ Q,
                                                             const __bf16 *__restrict__ K,
                                                             const __bf16 *__restrict__ V,
                                                             const __bf16 *__restrict__ dO,
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(NW * 64) PCOPS_DKV_OCC void attn_dkv2_kernel(const 
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
       kf[s] = kv ? *reinterpret_cast<const bf16x8 *>(kr0 + 16 * s) : bf16x8{};
-      vf[s] = kv ? *reinterpret_cast<const bf16x8 *>(vr0 + 16 * s) : bf16x8{};
+      vf[s] = (kv && MODE != 1) ? *reinterpret_cast<const bf16x8 *>(vr0 + 16 * s) : bf16x8{};
     }
   }
   const __bf16 *Qb = Q + st.q_off(bh);
@@ -755,8 +755,10 @@ __global__ __launch_bounds__(NW * 64) PCOPS_DKV_OCC void attn_dkv2_kernel(const 
     f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
     k_product<D>(S0, cq, kf);                 // S  (queries x keys)
     k_product<D>(S1, cq + 32 * C::kKS, kf);
-    k_product<D>(G0, cg, vf);                 // dP (queries x keys)
-    k_product<D>(G1, cg + 32 * C::kVS, vf);
+    if (MODE != 1) {
+      k_product<D>(G0, cg, vf);               // dP (queries x keys)
+      k_product<D>(G1, cg + 32 * C::kVS, vf);
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = acc_row(r, h);
@@ -764,13 +766,19 @@ __global__ __launch_bounds__(NW * 64) PCOPS_DKV_OCC void attn_dkv2_kernel(const 
       const float p1 = exp2f(__builtin_fmaf(S1[r], sl2, -cl[row + 32]));
       S0[r] = p0;
       S1[r] = p1;
-      G0[r] = p0 * (G0[r] - cd[row]);
-      G1[r] = p1 * (G1[r] - cd[row + 32]);
+      if (MODE != 1) {
+        G0[r] = p0 * (G0[r] - cd[row]);
+        G1[r] = p1 * (G1[r] - cd[row + 32]);
+      }
     }
-    v_product<D>(Y1, cg, S0);  // dV^T += dO^T P
-    v_product<D>(Y1, cg + 32 * C::kVS, S1);
-    v_product<D>(Y2, cq, G0);  // dK^T += Q^T dS
-    v_product<D>(Y2, cq + 32 * C::kKS, G1);
+    if (MODE != 2) {
+      v_product<D>(Y1, cg, S0);  // dV^T += dO^T P
+      v_product<D>(Y1, cg + 32 * C::kVS, S1);
+    }
+    if (MODE != 1) {
+      v_product<D>(Y2, cq, G0);  // dK^T += Q^T dS
+      v_product<D>(Y2, cq + 32 * C::kKS, G1);
+    }
     if (t + 1 < ntiles) {
       fwd2_store<D, NW>(sq + (cur ^ 1) * C::kKBuf, sg + (cur ^ 1) * C::kVBuf, qr, gr);
       if (threadIdx.x < kKT) {
@@ -780,8 +788,8 @@ __global__ __launch_bounds__(NW * 64) PCOPS_DKV_OCC void attn_dkv2_kernel(const 
     }
     lds_barrier();
   }
-  store_Y<__bf16, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
-  store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
+  if (MODE != 2) store_Y<__bf16, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
+  if (MODE != 1) store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
 }
 
 template <int D, int NW>
@@ -800,18 +808,46 @@ int launch_dq2(const void *q, const void *k, const void *v, const void *dout, co
   return PCOPS_OK;
 }
 
+bool dkv_split() {  // PCOPS_DKV_SPLIT=0 keeps the one-pass dK/dV kernel for D = 128 (A/B runs)
+  static const bool v = [] {
+    const char *e = getenv("PCOPS_DKV_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <int D, int NW>
 int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                 void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
   const size_t lds = C::kLds + 4 * kKT * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW>,
+  const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
+  if (D >= 128 && dkv_split()) {
+    // 8 waves per block halve each thread's share of the tile prefetch
+    using C8 = Fwd2Cfg<D, 8>;
+    const size_t lds8 = C8::kLds + 4 * kKT * sizeof(float);
+    const dim3 grid8((Lk + 8 * 32 - 1) / (8 * 32), BH);
+    static const hipError_t a1 = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, 8, 1, 2>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
+    static const hipError_t a2 = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, 8, 2, 2>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
+    if (a1 != hipSuccess || a2 != hipSuccess) return PCOPS_ERR_LAUNCH;
+    hipLaunchKernelGGL((attn_dkv2_kernel<D, 8, 1, 2>), grid8, dim3(C8::kThr), lds8, s, (const __bf16 *)q,
+                       (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
+                       (__bf16 *)dv, Lq, Lk, scale, st);
+    PC_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attn_dkv2_kernel<D, 8, 2, 2>), grid8, dim3(C8::kThr), lds8, s, (const __bf16 *)q,
+                       (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
+                       (__bf16 *)dv, Lq, Lk, scale, st);
+    PC_CHECK_LAUNCH();
+    return PCOPS_OK;
+  }
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW, 0, 1>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
-  const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q, (const __bf16 *)k,
-                     (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk, (__bf16 *)dv, Lq, Lk, scale,
-                     st);
+  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, 0, 1>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
+                     (__bf16 *)dv, Lq, Lk, scale, st);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

@@ -38,7 +38,7 @@ def max_over_neighbours(x):
     same max (same values, same first-index argmax for the backward) is taken
     over dim 2 of the contiguous (B, S, K, C) view instead."""
     if x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last):
-        return torch.max(x.permute(0, 2, 3, 1), dim=2)[0].permute(0, 2, 1)
+        return torch.max(x.permute(0, 2, 3, 1), dim=2)[0].permute(0, 2, 1).contiguous()
     return torch.max(x, 3)[0]
 
 

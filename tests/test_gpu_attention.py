@@ -18,6 +18,7 @@ SHAPES = [  # (B, H, Lq, Lk, E)
     (1, 8, 512, 512, 768),  # refine1 (hd 96)
     (1, 8, 200, 77, 512),   # ragged cross (hd 64)
     (1, 8, 2048, 512, 512), # refine2 cross
+    (1, 8, 333, 250, 1024), # ragged hd 128 (split dK/dV path)
     (2, 2, 70, 130, 64),    # hd 32
 ]
 
