@@ -117,34 +117,6 @@ def synth_55(B, seed, device, n_gt=8192):
     return partial.contiguous().to(device), gt.contiguous().to(device)
 
 
-class GradBucket:
-    """All parameter gradients as views of ONE flat fp32 buffer.
-
-    Batch-partitioned data parallelism needs exactly one exchange per step:
-    the gradient all-reduce, here a single RCCL all_reduce over the whole
-    232 MB bucket (ring, one call, no per-parameter launches).  The views keep
-    each parameter's strides (channels_last conv weights), so the fused Adam
-    kernel sees grads laid out like their params.  Parameters that never get
-    a gradient (the BatchNorms of the if_bn=False Conv2d blocks) keep a zero
-    one, which leaves them unchanged under Adam, as a None grad would."""
-
-    def __init__(self, params, device):
-        params = list(params)
-        self.flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=device)
-        off = 0
-        for p in params:
-            p.grad = self.flat[off:off + p.numel()].as_strided(p.shape, p.stride())
-            off += p.numel()
-
-    def zero(self):
-        self.flat.zero_()
-
-    def allreduce(self, world):
-        if world > 1:
-            dist.all_reduce(self.flat)
-            self.flat.mul_(1.0 / world)
-
-
 # ------------------------------------------------------------------ roofline model
 ATTN_ARGS = {"attention forward": 5, "attention bwd dq": 6, "attention bwd dkv": 7}
 
@@ -365,8 +337,31 @@ def setup_tunableop(mode, model, rank):
 
 
 # ------------------------------------------------------------------ main
+_PHASE = ["start"]
+
+
+def progress(msg):
+    """One stderr line per phase: long phases stay visibly alive, and a stall names its phase."""
+    _PHASE[0] = msg
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def heartbeat(every=30.0):
+    """A daemon thread repeating the current phase (MIOpen's first-run kernel
+    compilation and GEMM tuning are silent for minutes on a fresh box)."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(every)
+            print(f"[bench {time.strftime('%H:%M:%S')}] ... {_PHASE[0]}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     args = parse()
+    heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -381,6 +376,7 @@ def main():
 
     import svdformer_pointsea_amd as pkg
     from svdformer_pointsea_amd import _lib
+    from svdformer_pointsea_amd.train import FlatParams
 
     pkg.lib()  # fail loudly if libpcops.so is missing
     tuned = setup_tunableop(args.tunableop, args.model, rank)
@@ -390,7 +386,10 @@ def main():
     torch.manual_seed(0)  # identical init on every rank
     model = wl.Model(wl.cfg).to(device)
     nparams = sum(p.numel() for p in model.parameters())
-    bucket = GradBucket(model.parameters(), device)
+    amp = not args.fp32
+    # flat fp32 master weights + gradient bucket, bf16 shadows of the GEMM/conv
+    # weights refreshed by one cast per step (svdformer_pointsea_amd/train.py)
+    fp = FlatParams(model, device, bf16=amp)
     use_graph = not args.no_graph
     opt = wl.optimizer(model.parameters(), fused=True, capturable=use_graph)
     partial, gt = wl.synth(args.batch, 1000 + rank, device)
@@ -398,10 +397,11 @@ def main():
     # draws come from the device's default generator (graph-capturable)
     crop_rng = torch.cuda.default_generators[device.index] if args.model == "pointsea" else None
     loss_acc = torch.zeros((), device=device)
-    amp = not args.fp32
+    progress(f"{args.model}: {nparams} parameters; eager warm-up (MIOpen algorithm search)")
 
     def fwd_bwd():
-        bucket.zero()
+        fp.zero_grad()
+        fp.refresh()
         # the loss's gt FPS chain depends on gt only: it runs on a second
         # stream beside the whole forward pass (FPS occupies B CUs)
         with _lib.fork(device, lane=1) as br:
@@ -409,14 +409,15 @@ def main():
         inp = wl.inputs(partial, gt, crop_rng)
         depth = wl.images(inp)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=not use_graph):
-            pcds = model(inp, depth)
+            pcds = fp.forward(inp, depth)
             loss = wl.loss(pcds, inp, gt, br.join(*gts))
         loss.backward()
+        fp.collect()
         loss_acc.add_(loss.detach())  # logged without a host sync
 
     def eager_step():
         fwd_bwd()
-        bucket.allreduce(world)
+        fp.allreduce(world)
         opt.step()
 
     if use_graph:
@@ -432,6 +433,7 @@ def main():
                 eager_step()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        progress("eager warm-up done; capturing the step")
         g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
             fwd_bwd()
@@ -440,7 +442,7 @@ def main():
 
         def step():
             g_fb.replay()
-            bucket.allreduce(world)
+            fp.allreduce(world)
             g_opt.replay()
         span_steps = args.timing_steps
     else:
@@ -454,6 +456,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    progress(f"timing {args.steps} steps")
     t0 = time.perf_counter()
     host = 0.0  # time the host spends issuing a step (launches are asynchronous)
     for _ in range(args.steps):
@@ -532,6 +535,7 @@ def main():
                                   **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {})}
                               for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
         if world == 1 and not args.no_cpu_baseline:
+            progress(f"timed {out['ms_per_step']:.2f} ms/step; CPU baseline")
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_steps)
         print(json.dumps(out), flush=True)
     if world > 1:

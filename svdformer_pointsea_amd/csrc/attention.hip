@@ -796,7 +796,7 @@ template <int D, int NW>
 int launch_dq2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                void *dq, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
-  constexpr int OCC = D <= 96 ? 2 : 1;
+  constexpr int OCC = (D <= 96 || NW == 8) ? 2 : 1;
   static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
@@ -865,7 +865,8 @@ int dq2_dispatch(const void *q, const void *k, const void *v, const void *dout, 
     case 96:
       return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
     case 128:
-      return launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+      return wide ? launch_dq2<128, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s)
+                  : launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
     default:
       return PCOPS_ERR_UNSUPPORTED;
   }

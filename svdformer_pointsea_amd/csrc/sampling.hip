@@ -13,6 +13,7 @@
 // Index parity with sampling_gpu.cu:69-173 is bit-exact (same fused distance,
 // same tie order, same |p|^2 <= 1e-3 skip).
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 
 #include "common.h"
@@ -62,7 +63,13 @@ __device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
 // of the ballot (s_ff1), and across waves the order key is r' = r*SPLIT + h.
 // The cross-wave step packs (distance bits, 1023 - r', k) into one 64-bit
 // key and max-reduces the <= 16 per-wave slots with DPP in one row of lanes.
-template <int PPT>
+// ALLRED: after the one barrier every wave reduces the (round-parity double
+// buffered) slots itself, so the centre arrives without the leader wave's
+// second barrier and LDS round trip; ALLRED = false is the leader-wave form.
+// Measured: ALLRED wins with 8 waves (32x2048->512: 0.318 -> 0.307 ms) and
+// loses with 16, where 16 concurrent reductions contend for the VALU
+// (32x16384->2048: 2.78 -> 2.91 ms), so 16-wave blocks keep the leader.
+template <int PPT, bool ALLRED>
 __global__ __launch_bounds__(1024) void fps_reg_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
                                                         int NWT, int SPLIT, int *__restrict__ idx) {
   const int b = blockIdx.x;
@@ -96,12 +103,12 @@ __global__ __launch_bounds__(1024) void fps_reg_kernel(const float *__restrict__
     }
   }
   // per-wave slots: key (hi, lo) + coords; the leader wave's result
-  __shared__ uint2 skey[16];
-  __shared__ float4 sxyz[16];
+  __shared__ uint2 skey2[2][16];
+  __shared__ float4 sxyz2[2][16];
   __shared__ float4 sres;
-  if (t < 16) {
-    skey[t] = make_uint2(0u, 0u);  // absent waves never win
-    sxyz[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < 32) {
+    skey2[t >> 4][t & 15] = make_uint2(0u, 0u);  // absent waves never win
+    sxyz2[t >> 4][t & 15] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
 
@@ -110,6 +117,8 @@ __global__ __launch_bounds__(1024) void fps_reg_kernel(const float *__restrict__
   if (t == 0 && M > 0) out[0] = 0;
   FPS_STAMP_DECL
   for (int j = 1; j < M; ++j) {
+    uint2 *skey = skey2[ALLRED ? (j & 1) : 0];
+    float4 *sxyz = sxyz2[ALLRED ? (j & 1) : 0];
     // sweep: 8 VALU ops / point, no compare/select chain -- the lane only
     // tracks its max; the winning slot is recovered once per wave below.
     int best = kNeverBits;
@@ -146,7 +155,8 @@ __global__ __launch_bounds__(1024) void fps_reg_kernel(const float *__restrict__
     FPS_STAMP(1)
     lds_barrier();
     FPS_STAMP(2)
-    if (w == 0) {  // leader wave: 64-bit max over the <= 16 slots in one DPP row
+    float4 rv;
+    if (ALLRED || w == 0) {  // 64-bit max over the <= 16 slots in one DPP row
       const uint2 kv = skey[lane & 15];
       const float4 cv = sxyz[lane & 15];
       unsigned long long key = ((unsigned long long)kv.x << 32) | kv.y;
@@ -167,13 +177,25 @@ __global__ __launch_bounds__(1024) void fps_reg_kernel(const float *__restrict__
       if ((int)(ghi ^ 0x80000000u) != kNeverBits) {
         const int gw = (int)((glo >> 14) & 15u);  // winning wave == its slot lane
         const int k = (int)(glo & 0x3FFFu);
-        if (lane == gw) sres = make_float4(cv.x, cv.y, cv.z, __int_as_float(k));
-      } else if (lane == 0) {  // no valid point at all: the reference's dists_i[0] == 0
-        sres = make_float4(x0, y0, z0, __int_as_float(0));
+        if constexpr (ALLRED) {
+          rv = make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.x), gw)),
+                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.y), gw)),
+                           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.z), gw)), __int_as_float(k));
+        } else if (lane == gw) {
+          sres = make_float4(cv.x, cv.y, cv.z, __int_as_float(k));
+        }
+      } else {  // no valid point at all: the reference's dists_i[0] == 0
+        if constexpr (ALLRED) {
+          rv = make_float4(x0, y0, z0, __int_as_float(0));
+        } else if (lane == 0) {
+          sres = make_float4(x0, y0, z0, __int_as_float(0));
+        }
       }
     }
-    lds_barrier();
-    const float4 rv = sres;
+    if constexpr (!ALLRED) {
+      lds_barrier();
+      rv = sres;
+    }
     ox = rv.x;
     oy = rv.y;
     oz = rv.z;
@@ -299,6 +321,14 @@ int opt_n_threads(int work_size) {  // cuda_utils.h:15-19
   return t > 512 ? 512 : (t < 1 ? 1 : t);
 }
 
+bool fps_v1() {  // PCOPS_FPS_V1=1: leader-wave slot reduction (A/B runs)
+  static const bool v = [] {
+    const char *e = getenv("PCOPS_FPS_V1");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 unsigned grid_for(size_t total, int block) {
   size_t g = (total + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -331,8 +361,12 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
     const int nwt = nthreads / 64;
 #define FPS_CASE(P)                                                                                       \
   if (per <= P) {                                                                                         \
-    hipLaunchKernelGGL(fps_reg_kernel<P>, dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt, split, \
-                       idx);                                                                              \
+    if (fps_v1() || nthreads * split > 512)                                                               \
+      hipLaunchKernelGGL((fps_reg_kernel<P, false>), dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt, \
+                         split, idx);                                                                     \
+    else                                                                                                  \
+      hipLaunchKernelGGL((fps_reg_kernel<P, true>), dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt,  \
+                         split, idx);                                                                     \
     PC_CHECK_LAUNCH();                                                                                    \
     return PCOPS_OK;                                                                                      \
   }

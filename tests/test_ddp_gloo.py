@@ -1,8 +1,9 @@
 """World-size-2 gloo run of bench.py's data-parallel path on CPU.
 
 Each rank runs the real SVDFormer PCN step on its own sample (point ops on
-the oracle CPU path) with bench.GradBucket: gradients accumulate into one flat
-buffer whose all-reduce is the step's only collective.  After it, the
+the oracle CPU path) with train.FlatParams (bench.py's parameter storage):
+gradients accumulate into one flat buffer whose all-reduce is the step's
+only collective.  After it, the
 gradients must be identical on both ranks and equal the mean of the ranks'
 local gradients, and one Adam step must leave identical weights."""
 import os
@@ -24,34 +25,36 @@ def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from bench import GradBucket, synth_pcn
+    from bench import synth_pcn
+    from svdformer_pointsea_amd.train import FlatParams
     from oracle.cpu_path import cpu_ops, depth_images
     from svdformer_pointsea_amd.render import PCViews
     from svdformer_pointsea_amd.svdformer import Model, PCNConfig, get_loss
 
     torch.manual_seed(0)
     model = Model(PCNConfig)
-    bucket = GradBucket(model.parameters(), "cpu")
+    fp = FlatParams(model, "cpu", bf16=False)
     partial, gt = synth_pcn(1, 1000 + rank, "cpu")
     render = PCViews(TRANS=-0.7, RESOLUTION=224)
     with cpu_ops():
         depth = depth_images(render, partial).unsqueeze(1)
-        bucket.zero()
-        loss, _ = get_loss(model(partial, depth), gt)
+        fp.zero_grad()
+        loss, _ = get_loss(fp.forward(partial, depth), gt)
         loss.backward()
-    local = bucket.flat.clone()
-    bucket.allreduce(world)
+        fp.collect()
+    local = fp.grad.clone()
+    fp.allreduce(world)
     mean_local = local.clone()
     dist.all_reduce(mean_local)
     mean_local /= world
-    other = bucket.flat.clone()
+    other = fp.grad.clone()
     dist.broadcast(other, src=0)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     opt.step()
     w = torch.cat([p.detach().flatten() for p in model.parameters()])
     w0 = w.clone()
     dist.broadcast(w0, src=0)
-    out[rank] = (float((bucket.flat - mean_local).abs().max()), float((bucket.flat - other).abs().max()),
+    out[rank] = (float((fp.grad - mean_local).abs().max()), float((fp.grad - other).abs().max()),
                  float(local.abs().max()), float((w - w0).abs().max()))
     dist.destroy_process_group()
 

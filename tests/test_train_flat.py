@@ -1,0 +1,42 @@
+"""train.FlatParams: bf16 shadows + flat fp32 master/gradient buffers give
+exactly the gradients of plain torch.autocast (CPU autocast, bf16)."""
+import copy
+
+import torch
+from torch import nn
+
+from svdformer_pointsea_amd.train import FlatParams
+
+
+class _Net(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv1d(8, 16, 1)
+        self.norm = nn.LayerNorm(16)
+        self.lin = nn.Linear(16, 4)
+
+    def forward(self, x):
+        y = self.conv(x).transpose(1, 2)
+        return self.lin(self.norm(y.float())).float().square().mean()
+
+
+def test_flat_params_match_autocast_grads():
+    torch.manual_seed(0)
+    a = _Net()
+    b = copy.deepcopy(a)
+    x = torch.randn(3, 8, 5)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        a(x).backward()
+    fp = FlatParams(b, "cpu")
+    fp.zero_grad()
+    fp.refresh()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        fp.forward(x).backward()
+    fp.collect()
+    assert fp.n16 == sum(p.numel() for n, p in b.named_parameters() if not n.startswith("norm"))
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert pb.grad.dtype == torch.float32
+        assert torch.equal(pa.grad, pb.grad), n
+        assert torch.equal(pa.data, pb.data), n
+    # the fp32 master weights are the parameters themselves (views of one buffer)
+    assert all(p.data_ptr() >= fp.flat.data_ptr() for p in b.parameters())
