@@ -45,6 +45,51 @@ def _vptr(t, off=0):
     return ctypes.c_void_p(t.data_ptr() + off * t.element_size())
 
 
+# ------------------------------------------------------------------ linear layers
+class _Linear(Function):
+    """F.linear (hipBLASLt GEMM + bias) whose bias gradient is pcops_bias_grad
+    (one deterministic pass over the output gradient) instead of torch's
+    separate per-layer bf16 reduction; the input / weight gradients are the
+    same two GEMMs torch's linear backward issues.  Under autocast the inputs
+    are cast to bf16 like F.linear's autocast rule."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.bdt = b.dtype
+        return F.linear(x, w, b)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        C = g.shape[-1]
+        g2 = g.reshape(-1, C).contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (g2 @ w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            gw = g2.t() @ x.reshape(-1, x.shape[-1])
+        if ctx.needs_input_grad[2]:
+            gb = torch.empty(C, dtype=ctx.bdt, device=g.device)
+            wsb = lib().pcops_bias_grad_workspace_bytes(g2.shape[0], C)
+            ws = _lib.Workspace.get(g.device, wsb)
+            with torch.cuda.device(g.device):
+                call("bias_grad", lib().pcops_bias_grad, ptr(g2), _dt(g2), g2.shape[0], C, ptr(gb), _DT[ctx.bdt],
+                     ptr(ws), wsb, stream_of(g2))
+        return gx, gw, gb
+
+
+def linear(x, w, b=None):
+    """F.linear for the blocks' Linear / 1x1-conv layers (see _Linear)."""
+    C = w.shape[0]
+    if (b is None or not x.is_cuda or C % 8 or C > 2048 or x.dtype not in _DT or w.dtype not in _DT
+            or b.dtype not in _DT or not torch.is_grad_enabled()):
+        return F.linear(x, w, b)
+    return _Linear.apply(x, w, b)
+
+
 # ------------------------------------------------------------------ attention core
 def _layout(t, batch_first):
     """(sb, srow) element strides of a (B, L, W) / (L, B, W) tensor."""
@@ -168,7 +213,7 @@ class MultiheadAttention(nn.Module):
 
     def _proj(self, x, r0, r1):
         b = None if self.in_proj_bias is None else self.in_proj_bias[r0:r1]
-        return F.linear(x, self.in_proj_weight[r0:r1], b)
+        return linear(x, self.in_proj_weight[r0:r1], b)
 
     def forward(self, query, key, value, need_weights=True):
         E, H = self.embed_dim, self.num_heads
@@ -189,7 +234,7 @@ class MultiheadAttention(nn.Module):
         if dt is not None and any(s.dtype != dt for s in srcs):
             srcs = tuple(s.to(dt) for s in srcs)
         o = AttentionCore.apply((H, scale, E, self.batch_first, *wins), *srcs)
-        return self.out_proj(o), None
+        return linear(o, self.out_proj.weight, self.out_proj.bias), None
 
 
 # ------------------------------------------------------------------ fused block glue
@@ -300,7 +345,7 @@ def layer_norm(norm, a, b=None):
 
 def _conv1x1_tokens(conv, x_tok):
     """Conv1d(k=1) applied to token-major (B, L, C_in) input as a GEMM."""
-    return F.linear(x_tok, conv.weight.view(conv.weight.shape[0], -1), conv.bias)
+    return linear(x_tok, conv.weight.view(conv.weight.shape[0], -1), conv.bias)
 
 
 class _BlockBase(nn.Module):
@@ -329,7 +374,8 @@ class _BlockBase(nn.Module):
     def _tail(self, s1, attn):
         """norm12(s1 + attn) -> FFN -> (residual stream fp32, FFN output)."""
         s2, s2h = layer_norm(self.norm12, s1, attn)
-        f = self.linear12(self.activation1(self.linear11(s2h)))
+        h = self.activation1(linear(s2h, self.linear11.weight, self.linear11.bias))
+        f = linear(h, self.linear12.weight, self.linear12.bias)
         return s2, f
 
     def _in(self, x_tok):

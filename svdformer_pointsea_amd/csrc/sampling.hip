@@ -70,7 +70,7 @@ __device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
 // loses with 16, where 16 concurrent reductions contend for the VALU
 // (32x16384->2048: 2.78 -> 2.91 ms), so 16-wave blocks keep the leader.
 template <int PPT, bool ALLRED>
-__global__ __launch_bounds__(1024) void fps_reg_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
+__global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
                                                         int NWT, int SPLIT, int *__restrict__ idx) {
   const int b = blockIdx.x;
   const float *p = xyz + (size_t)b * N * 3;
@@ -329,6 +329,14 @@ bool fps_v1() {  // PCOPS_FPS_V1=1: leader-wave slot reduction (A/B runs)
   return v;
 }
 
+int fps_split_ppt() {  // PCOPS_FPS_SPLIT_PPT: points per reference thread above which 1024 threads are used
+  static const int v = [] {
+    const char *e = getenv("PCOPS_FPS_SPLIT_PPT");
+    return e ? atoi(e) : 16;
+  }();
+  return v;
+}
+
 unsigned grid_for(size_t total, int block) {
   size_t g = (total + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -354,9 +362,10 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
   const int ppt = (N + T - 1) / T;  // points per reference thread
   hipStream_t s = (hipStream_t)stream;
   if (ppt <= kFpsMaxPPT) {
-    // clouds with > 8 points per reference thread use 2 hardware threads per
-    // reference thread (1024 threads, 4 waves / SIMD) for latency hiding
-    const int split = (ppt > 8 && T == 512) ? 2 : 1;
+    // clouds with > 16 points per reference thread use 2 hardware threads per
+    // reference thread (1024 threads, 4 waves / SIMD).  Up to 16 the 8-wave
+    // block wins: 32x8192->2048 2.41 -> 2.06 ms (fewer slots, one barrier).
+    const int split = (ppt > fps_split_ppt() && T == 512) ? 2 : 1;
     const int per = (ppt + split - 1) / split;
     const int nwt = nthreads / 64;
 #define FPS_CASE(P)                                                                                       \
@@ -375,6 +384,7 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
     FPS_CASE(4)
     FPS_CASE(8)
     FPS_CASE(16)
+    FPS_CASE(32)
 #undef FPS_CASE
   }
   if (!workspace || workspace_bytes < pcops_fps_workspace_bytes(B, N)) return PCOPS_ERR_WORKSPACE;

@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import SDG_Decoder, cross_attention, self_attention, to_channels, to_tokens
+from .attention import SDG_Decoder, cross_attention, linear, self_attention, to_channels, to_tokens
 from .chamfer3D import chamfer_3DDist
 from .model_utils import fps_subsample, group_local, sample_and_group_knn
 from ._lib import fork
@@ -28,7 +28,7 @@ from .pointnet2_utils import furthest_point_sample, gather_operation
 
 def _lin(conv, x):
     """A kernel-size-1 Conv1d applied to token-major (..., C_in) rows as a GEMM."""
-    return F.linear(x, conv.weight.view(conv.weight.shape[0], -1), conv.bias)
+    return linear(x, conv.weight.view(conv.weight.shape[0], -1), conv.bias)
 
 
 def max_over_neighbours(x):

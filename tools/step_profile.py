@@ -14,7 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from torch.profiler import ProfilerActivity, profile
 
-from bench import Workload
+from bench import Workload, setup_tunableop
+from svdformer_pointsea_amd import _lib
+from svdformer_pointsea_amd.train import FlatParams
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="svdformer")
@@ -23,22 +25,28 @@ ap.add_argument("--rows", type=int, default=40)
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.backends.cudnn.benchmark = True
+setup_tunableop("use", args.model, 0)
 wl = Workload(args.model)
 B = args.batch or wl.batch
 torch.manual_seed(0)
 model = wl.Model(wl.cfg).to(dev)
+fp = FlatParams(model, dev)
 opt = wl.optimizer(model.parameters(), fused=True)
 partial, gt = wl.synth(B, 1000, dev)
 rng = torch.cuda.default_generators[0] if args.model == "pointsea" else None
 
 
-def step():
+def step():  # bench.py's eager step
+    fp.zero_grad()
+    fp.refresh()
+    with _lib.fork(dev, lane=1) as br:
+        gts = wl.gt_pyramid(gt)
     inp = wl.inputs(partial, gt, rng)
     depth = wl.images(inp)
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        loss = wl.loss(model(inp, depth), inp, gt)
-    opt.zero_grad(set_to_none=True)
+        loss = wl.loss(fp.forward(inp, depth), inp, gt, br.join(*gts))
     loss.backward()
+    fp.collect()
     opt.step()
 
 
