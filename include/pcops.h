@@ -193,6 +193,20 @@ unsigned long long pcops_bias_grad_workspace_bytes(int rows, int C);
 int pcops_bias_grad(const void *g, int g_dtype, int rows, int C, void *out, int out_dtype, void *workspace,
                     unsigned long long workspace_bytes, pcops_stream_t stream);
 
+/* ---------------- PCSA spectral gating (models/model_utils.py:358-430) ----------------
+ * Per patch p (= b*S + s) of K neighbours x C channels stored [p][k][c] (the
+ * channels_last memory order of the (B, C, S, K) conv output):
+ *   out[p] = D^T diag(gates[p]) D x[p]      (D = basis, K x K row-major fp32)
+ * pcops_pcsa_backward: dx[p] = (D^T diag(g) D)^T dout[p];
+ *   dgates[p][k] = sum_c (D dout[p])[k][c] * (D x[p])[k][c].
+ * dtype codes 0 = fp32, 1 = bf16 (x, out, dx share x_dtype; dgates has
+ * gates_dtype).  K in {4, 8, 16, 32}. */
+int pcops_pcsa_forward(const void *x, int x_dtype, const void *gates, int gates_dtype, const float *basis, int patches,
+                       int K, int C, void *out, pcops_stream_t stream);
+int pcops_pcsa_backward(const void *x, int x_dtype, const void *dout, int dout_dtype, const void *gates,
+                        int gates_dtype, const float *basis, int patches, int K, int C, void *dx, void *dgates,
+                        pcops_stream_t stream);
+
 /* ---------------- depth renderers ----------------
  * PCViews.get_img (models/model_utils.py:1196-1234 -> points2depth :1080-1115 ->
  * distribute :1004-1077, size 1): points (B,N,3); rot (V,3,3) row-major =

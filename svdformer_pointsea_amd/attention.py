@@ -81,11 +81,19 @@ class _Linear(Function):
         return gx, gw, gb
 
 
+# Measured on the PCN step: torch's per-layer bf16 reduction (3.3 ms / 115
+# launches) beats pcops_bias_grad's two-stage form (7.4 ms: its column pass
+# is latency-bound), so the blocks keep F.linear; _Linear stays available
+# for the fused form (bias gradient folded into the LayerNorm / GELU
+# backward passes) that is the next step.
+USE_FUSED_BIAS_GRAD = False
+
+
 def linear(x, w, b=None):
     """F.linear for the blocks' Linear / 1x1-conv layers (see _Linear)."""
     C = w.shape[0]
-    if (b is None or not x.is_cuda or C % 8 or C > 2048 or x.dtype not in _DT or w.dtype not in _DT
-            or b.dtype not in _DT or not torch.is_grad_enabled()):
+    if (not USE_FUSED_BIAS_GRAD or b is None or not x.is_cuda or C % 8 or C > 2048 or x.dtype not in _DT
+            or w.dtype not in _DT or b.dtype not in _DT or not torch.is_grad_enabled()):
         return F.linear(x, w, b)
     return _Linear.apply(x, w, b)
 

@@ -752,32 +752,44 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
     const __bf16 *cg = sg + cur * C::kVBuf;
     const float *cl = slse + cur * kKT;
     const float *cd = sdl + cur * kKT;
-    f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
-    k_product<D>(S0, cq, kf);                 // S  (queries x keys)
-    k_product<D>(S1, cq + 32 * C::kKS, kf);
-    if (MODE != 1) {
-      k_product<D>(G0, cg, vf);               // dP (queries x keys)
+    if constexpr (MODE == 0) {
+      f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
+      k_product<D>(S0, cq, kf);  // S  (queries x keys)
+      k_product<D>(S1, cq + 32 * C::kKS, kf);
+      k_product<D>(G0, cg, vf);  // dP (queries x keys)
       k_product<D>(G1, cg + 32 * C::kVS, vf);
-    }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = acc_row(r, h);
-      const float p0 = exp2f(__builtin_fmaf(S0[r], sl2, -cl[row]));  // 0 for rows beyond Lq (lse = +inf)
-      const float p1 = exp2f(__builtin_fmaf(S1[r], sl2, -cl[row + 32]));
-      S0[r] = p0;
-      S1[r] = p1;
-      if (MODE != 1) {
+      for (int r = 0; r < 16; ++r) {
+        const int row = acc_row(r, h);
+        const float p0 = exp2f(__builtin_fmaf(S0[r], sl2, -cl[row]));  // 0 for rows beyond Lq (lse = +inf)
+        const float p1 = exp2f(__builtin_fmaf(S1[r], sl2, -cl[row + 32]));
+        S0[r] = p0;
+        S1[r] = p1;
         G0[r] = p0 * (G0[r] - cd[row]);
         G1[r] = p1 * (G1[r] - cd[row + 32]);
       }
-    }
-    if (MODE != 2) {
       v_product<D>(Y1, cg, S0);  // dV^T += dO^T P
       v_product<D>(Y1, cg + 32 * C::kVS, S1);
-    }
-    if (MODE != 1) {
       v_product<D>(Y2, cq, G0);  // dK^T += Q^T dS
       v_product<D>(Y2, cq + 32 * C::kKS, G1);
+    } else {
+      // one 32-query half at a time: half the live S / dP registers (the
+      // per-accumulator order -- half 0 then half 1 -- is unchanged)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        f32x16 S = f32x16{}, G = f32x16{};
+        k_product<D>(S, cq + 32 * hf * C::kKS, kf);
+        if (MODE == 2) k_product<D>(G, cg + 32 * hf * C::kVS, vf);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = acc_row(r, h) + 32 * hf;
+          const float p = exp2f(__builtin_fmaf(S[r], sl2, -cl[row]));
+          S[r] = p;
+          if (MODE == 2) G[r] = p * (G[r] - cd[row]);
+        }
+        if (MODE == 1) v_product<D>(Y1, cg + 32 * hf * C::kVS, S);
+        if (MODE == 2) v_product<D>(Y2, cq + 32 * hf * C::kKS, G);
+      }
     }
     if (t + 1 < ntiles) {
       fwd2_store<D, NW>(sq + (cur ^ 1) * C::kKBuf, sg + (cur ^ 1) * C::kVBuf, qr, gr);
@@ -822,7 +834,7 @@ int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, c
   using C = Fwd2Cfg<D, NW>;
   const size_t lds = C::kLds + 4 * kKT * sizeof(float);
   const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
-  if (D >= 128 && dkv_split()) {
+  if (D >= 96 && dkv_split()) {
     // 8 waves per block halve each thread's share of the tile prefetch
     using C8 = Fwd2Cfg<D, 8>;
     const size_t lds8 = C8::kLds + 4 * kKT * sizeof(float);

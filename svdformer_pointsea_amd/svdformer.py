@@ -83,6 +83,40 @@ class MLP_CONV(nn.Module):
         return self.mlp(x)
 
 
+class _PCSAApply(torch.autograd.Function):
+    """PCSA's DCT -> gate -> inverse-DCT chain (model_utils.py:413-430) as one
+    libpcops pass per patch on the channels_last (B, C, S, K) features."""
+
+    @staticmethod
+    def forward(ctx, x, gates, dct):
+        from ._lib import call, lib, ptr, stream_of
+        gates = gates.contiguous()
+        basis = dct.float().contiguous()
+        B, C, S, K = x.shape
+        out = torch.empty_like(x)  # keeps channels_last
+        with torch.cuda.device(x.device):
+            call("pcsa_forward", lib().pcops_pcsa_forward, ptr(x), _DTC[x.dtype], ptr(gates), _DTC[gates.dtype],
+                 ptr(basis), B * S, K, C, ptr(out), stream_of(x))
+        ctx.save_for_backward(x, gates, basis)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import call, lib, ptr, stream_of
+        x, gates, basis = ctx.saved_tensors
+        B, C, S, K = x.shape
+        g = g.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x)
+        dgates = torch.empty_like(gates)
+        with torch.cuda.device(x.device):
+            call("pcsa_backward", lib().pcops_pcsa_backward, ptr(x), _DTC[x.dtype], ptr(g), _DTC[g.dtype],
+                 ptr(gates), _DTC[gates.dtype], ptr(basis), B * S, K, C, ptr(dx), ptr(dgates), stream_of(x))
+        return dx, dgates, None
+
+
+_DTC = {torch.float32: 0, torch.bfloat16: 1}
+
+
 class PCSA(nn.Module):
     """Point Cloud Spectral Adapter (model_utils.py:358-430): orthonormal DCT-II
     along the neighbourhood axis, channel-averaged frequency gates, inverse DCT."""
@@ -116,6 +150,11 @@ class PCSA(nn.Module):
             return x
         B, C, S, K = x.shape
         dct, idct = self._dct(x.device, x.dtype)
+        if (x.is_cuda and K in (4, 8, 16, 32) and x.dtype in (torch.float32, torch.bfloat16)
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            # one pass per (b, s) patch on libpcops (csrc/pcsa.hip): out = D^T diag(g) D x
+            gates = self.freq_mlp(x.mean(dim=1))
+            return _PCSAApply.apply(x, gates, dct)
         x_flat = x.permute(0, 2, 1, 3).contiguous().view(B * S * C, K)
         spec = torch.matmul(x_flat, dct.t())
         gates = self.freq_mlp(x.mean(dim=1)).view(B * S, K)

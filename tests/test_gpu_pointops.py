@@ -320,3 +320,30 @@ def test_pcviews_real_golden(dev):
     img = real.get_img(T(g["points"], dev)).cpu().numpy()
     np.testing.assert_allclose(img[:, 0], g["img0"], atol=1e-6)
     np.testing.assert_array_equal(img[:, 0], img[:, 2])
+
+
+@pytest.mark.parametrize("dtype,K,C", [(torch.float32, 16, 128), (torch.float32, 16, 256), (torch.bfloat16, 16, 128),
+                                       (torch.float32, 8, 64)])
+def test_pcsa_kernel_matches_torch_chain(dev, dtype, K, C):
+    """PCSA (model_utils.py:408-430): the libpcops patch kernel vs the
+    reference's permute / DCT matmul / gate / IDCT matmul chain, fwd + bwd."""
+    from svdformer_pointsea_amd.svdformer import PCSA
+
+    torch.manual_seed(K + C)
+    m = PCSA(C, K).to(dev)
+    B, S = 2, 37
+    x0 = torch.randn(B, C, S, K, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+    go = torch.randn(B, C, S, K, device=dev).to(dtype)
+    xa = x0.clone().requires_grad_(True)
+    ya = m(xa)                                     # kernel path (channels_last input)
+    (ya.float() * go.float()).sum().backward()
+    ga = [p.grad.clone() for p in m.parameters()]
+    m.zero_grad()
+    xb = x0.contiguous().clone().requires_grad_(True)
+    yb = m(xb)                                     # reference chain (NCHW input)
+    (yb.float() * go.float()).sum().backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 2e-5
+    torch.testing.assert_close(ya.float(), yb.float(), rtol=tol, atol=tol)
+    torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=tol, atol=tol)
+    for a, b in zip(ga, (p.grad for p in m.parameters())):
+        torch.testing.assert_close(a.float(), b.float(), rtol=tol * 5, atol=tol * 5)
