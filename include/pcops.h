@@ -184,15 +184,6 @@ int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int 
                         void *dx16, float *dgamma, float *dbeta, void *workspace, unsigned long long workspace_bytes,
                         pcops_stream_t stream);
 
-/* pcops_bias_grad: out[c] = sum_r g[r][c] -- the bias gradient of the blocks'
- * Linear / 1x1-conv layers (nn.Linear.bias, nn.Conv1d.bias; torch's separate
- * per-layer reduction).  g (rows, C) row-major fp32 or bf16, C % 8 == 0,
- * C <= 2048, 16-B aligned rows; out (C) fp32 or bf16, overwritten.
- * Deterministic (fixed chunk order).  workspace: pcops_bias_grad_workspace_bytes. */
-unsigned long long pcops_bias_grad_workspace_bytes(int rows, int C);
-int pcops_bias_grad(const void *g, int g_dtype, int rows, int C, void *out, int out_dtype, void *workspace,
-                    unsigned long long workspace_bytes, pcops_stream_t stream);
-
 /* ---------------- PCSA spectral gating (models/model_utils.py:358-430) ----------------
  * Per patch p (= b*S + s) of K neighbours x C channels stored [p][k][c] (the
  * channels_last memory order of the (B, C, S, K) conv output):

@@ -46,18 +46,35 @@ def _vptr(t, off=0):
 
 
 # ------------------------------------------------------------------ linear layers
+def _wgrad(g2, x2, wdt):
+    """g2^T x2 for (T, Cout) x (T, Cin) with T = B*L tokens (up to 65536).
+
+    hipBLASLt tiles this long-K, small-output GEMM (e.g. 512 x 512 x 65536)
+    into a handful of workgroups (145-450 TFLOP/s).  Split-K instead: S
+    batched partial GEMMs over T/S-token slices with fp32 outputs
+    (torch.bmm(..., out_dtype=float32)), one fp32 sum, one rounding to the
+    weight dtype -- 2-4x faster at these shapes (tools/gemm_bench.py)."""
+    T, Cout = g2.shape
+    Cin = x2.shape[1]
+    S = 16 if Cout * Cin <= (2 << 20) else 4
+    while S > 1 and (T % S or T // S < 2048):
+        S //= 2
+    if S == 1 or g2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16:
+        return (g2.t() @ x2).to(wdt)
+    part = torch.bmm(g2.view(S, T // S, Cout).transpose(1, 2), x2.view(S, T // S, Cin), out_dtype=torch.float32)
+    return part.sum(0).to(wdt)
+
+
 class _Linear(Function):
-    """F.linear (hipBLASLt GEMM + bias) whose bias gradient is pcops_bias_grad
-    (one deterministic pass over the output gradient) instead of torch's
-    separate per-layer bf16 reduction; the input / weight gradients are the
-    same two GEMMs torch's linear backward issues.  Under autocast the inputs
-    are cast to bf16 like F.linear's autocast rule."""
+    """F.linear whose weight gradient is the split-K form of _wgrad; the input
+    gradient (g @ W) and the bias gradient (a column sum) are torch's.  Under
+    autocast the inputs are cast to bf16 like F.linear's autocast rule."""
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
-        ctx.bdt = b.dtype
+        ctx.has_b = b is not None
         return F.linear(x, w, b)
 
     @staticmethod
@@ -65,35 +82,21 @@ class _Linear(Function):
     def backward(ctx, g):
         x, w = ctx.saved_tensors
         C = g.shape[-1]
-        g2 = g.reshape(-1, C).contiguous()
+        g2 = g.reshape(-1, C)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = (g2 @ w).view(x.shape)
         if ctx.needs_input_grad[1]:
-            gw = g2.t() @ x.reshape(-1, x.shape[-1])
-        if ctx.needs_input_grad[2]:
-            gb = torch.empty(C, dtype=ctx.bdt, device=g.device)
-            wsb = lib().pcops_bias_grad_workspace_bytes(g2.shape[0], C)
-            ws = _lib.Workspace.get(g.device, wsb)
-            with torch.cuda.device(g.device):
-                call("bias_grad", lib().pcops_bias_grad, ptr(g2), _dt(g2), g2.shape[0], C, ptr(gb), _DT[ctx.bdt],
-                     ptr(ws), wsb, stream_of(g2))
+            gw = _wgrad(g2.contiguous(), x.reshape(-1, x.shape[-1]).contiguous(), w.dtype)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = g2.sum(0)
         return gx, gw, gb
 
 
-# Measured on the PCN step: torch's per-layer bf16 reduction (3.3 ms / 115
-# launches) beats pcops_bias_grad's two-stage form (7.4 ms: its column pass
-# is latency-bound), so the blocks keep F.linear; _Linear stays available
-# for the fused form (bias gradient folded into the LayerNorm / GELU
-# backward passes) that is the next step.
-USE_FUSED_BIAS_GRAD = False
-
-
 def linear(x, w, b=None):
-    """F.linear for the blocks' Linear / 1x1-conv layers (see _Linear)."""
-    C = w.shape[0]
-    if (not USE_FUSED_BIAS_GRAD or b is None or not x.is_cuda or C % 8 or C > 2048 or x.dtype not in _DT
-            or w.dtype not in _DT or b.dtype not in _DT or not torch.is_grad_enabled()):
+    """F.linear for the blocks' Linear / 1x1-conv layers: the _Linear path when
+    the weight gradient is a long-K GEMM (>= 8192 tokens), else F.linear."""
+    if not (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and x.numel() // x.shape[-1] >= 8192):
         return F.linear(x, w, b)
     return _Linear.apply(x, w, b)
 

@@ -276,62 +276,6 @@ int ln_bwd_blocks(int rows) { return (rows + kRowsPerBlock - 1) / kRowsPerBlock;
 bool dt_ok(int dt) { return dt == 0 || dt == 1; }
 
 
-// ---------------------------------------------------------------- bias gradient
-// db[c] = sum_r g[r][c] for the 1x1 conv / Linear layers of the blocks
-// (torch computes it as a separate bf16 reduction per layer).  Stage 1: a
-// block owns kBgRows rows; each thread sums 8 consecutive columns of every
-// (256 / (C/8))-th row in fp32 with 16-B loads, the block folds its row
-// groups in LDS and writes one fp32 partial row.  Stage 2: one thread per
-// column adds the partials in chunk order (deterministic) and writes db.
-constexpr int kBgRows = 256;
-
-__global__ __launch_bounds__(256) void bias_grad_partial_kernel(const void *__restrict__ g, int gdt, int rows, int C,
-                                                                float *__restrict__ part) {
-  __shared__ float red[256 * 8];
-  const int cv = C / 8;                   // 8-column vectors per row (<= 256)
-  const int groups = 256 / cv;            // row groups per block
-  const int t = threadIdx.x, v = t % cv, grp = t / cv;
-  const int r0 = blockIdx.x * kBgRows;
-  const int r1 = min(rows, r0 + kBgRows);
-  float acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  if (grp < groups) {
-    for (int r = r0 + grp; r < r1; r += groups) {
-      const long long i = (long long)r * C + 8 * v;
-      if (gdt == 0) {
-        const float4 a = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(g) + i);
-        const float4 b = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(g) + i + 4);
-        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
-      } else {
-        typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
-        const bf8 a = *reinterpret_cast<const bf8 *>(reinterpret_cast<const __bf16 *>(g) + i);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += (float)a[j];
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[t * 8 + j] = acc[j];
-  __syncthreads();
-  if (grp == 0) {
-    for (int o = 1; o < groups; ++o)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += red[(o * cv + v) * 8 + j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) part[(long long)blockIdx.x * C + 8 * v + j] = acc[j];
-  }
-}
-
-__global__ void bias_grad_final_kernel(const float *__restrict__ part, int chunks, int C, void *__restrict__ out,
-                                       int odt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int k = 0; k < chunks; ++k) s += part[(long long)k * C + c];
-  st(out, odt, c, s);
-}
 }  // namespace
 
 extern "C" int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype,
@@ -394,33 +338,6 @@ extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const vo
                      nullptr, nullptr, C);
   hipLaunchKernelGGL(ln_colsum_kernel, dim3((2 * C + 63) / 64, 1), dim3(256), 0, s, slice, slices, 2 * C, nullptr,
                      dgamma, dbeta, C);
-  PC_CHECK_LAUNCH();
-  return PCOPS_OK;
-}
-
-extern "C" unsigned long long pcops_bias_grad_workspace_bytes(int rows, int C) {
-  if (rows <= 0 || C <= 0) return 0;
-  return (unsigned long long)((rows + kBgRows - 1) / kBgRows) * C * sizeof(float);
-}
-
-extern "C" int pcops_bias_grad(const void *g, int g_dtype, int rows, int C, void *out, int out_dtype, void *workspace,
-                               unsigned long long workspace_bytes, pcops_stream_t stream) {
-  if (rows < 0 || C <= 0 || C % 8 != 0 || C > 2048 || (g_dtype != 0 && g_dtype != 1) ||
-      (out_dtype != 0 && out_dtype != 1))
-    return PCOPS_ERR_INVALID;
-  if (!out) return PCOPS_ERR_INVALID;
-  hipStream_t s = (hipStream_t)stream;
-  if (rows == 0) {
-    if (hipMemsetAsync(out, 0, (size_t)C * (out_dtype == 0 ? 4 : 2), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
-    return PCOPS_OK;
-  }
-  if (!g) return PCOPS_ERR_INVALID;
-  if (!workspace || workspace_bytes < pcops_bias_grad_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
-  const int chunks = (rows + kBgRows - 1) / kBgRows;
-  hipLaunchKernelGGL(bias_grad_partial_kernel, dim3(chunks), dim3(256), 0, s, g, g_dtype, rows, C, (float *)workspace);
-  PC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bias_grad_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, (const float *)workspace, chunks,
-                     C, out, out_dtype);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

@@ -334,13 +334,16 @@ def test_pcsa_kernel_matches_torch_chain(dev, dtype, K, C):
     B, S = 2, 37
     x0 = torch.randn(B, C, S, K, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
     go = torch.randn(B, C, S, K, device=dev).to(dtype)
+    amp = dtype == torch.bfloat16  # bf16 features only occur under autocast
     xa = x0.clone().requires_grad_(True)
-    ya = m(xa)                                     # kernel path (channels_last input)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        ya = m(xa)                                 # kernel path (channels_last input)
     (ya.float() * go.float()).sum().backward()
     ga = [p.grad.clone() for p in m.parameters()]
     m.zero_grad()
     xb = x0.contiguous().clone().requires_grad_(True)
-    yb = m(xb)                                     # reference chain (NCHW input)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        yb = m(xb)                                 # reference chain (NCHW input)
     (yb.float() * go.float()).sum().backward()
     tol = 2e-2 if dtype == torch.bfloat16 else 2e-5
     torch.testing.assert_close(ya.float(), yb.float(), rtol=tol, atol=tol)
