@@ -42,6 +42,28 @@ def max_over_neighbours(x):
     return torch.max(x, 3)[0]
 
 
+import os as _os
+
+# Which 1x1 convs run as GEMMs: "sa" (default) = the SA modules on the main
+# stream.  The local encoder's EdgeConvs run on a side stream (Model.forward)
+# beside hipBLASLt GEMMs of the main stream; hipBLASLt's stream-K kernels
+# synchronise workgroups through a shared workspace, and a graph replay with
+# GEMMs on both streams hung once (PointSea), so the EdgeConvs stay on MIOpen.
+_CONV1X1 = _os.environ.get("PCOPS_CONV1X1", "sa")  # all | edge | sa | off
+
+
+def conv1x1(x, conv, where="sa"):
+    """nn.Conv2d with a 1x1 kernel on channels_last (B, C, S, K) features, as
+    the GEMM it is over the (B, S, K, C) memory (hipBLASLt, split-K weight
+    gradient via attention.linear) instead of MIOpen's convolution; the result
+    is channels_last again.  Other convs go to MIOpen unchanged."""
+    if (_CONV1X1 in ("all", where) and x.is_cuda and x.dim() == 4 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.groups == 1 and x.is_contiguous(memory_format=torch.channels_last)):
+        y = linear(x.permute(0, 2, 3, 1), conv.weight.view(conv.out_channels, -1), conv.bias)
+        return y.permute(0, 3, 1, 2)
+    return conv(x)
+
+
 # ----------------------------------------------------------------- blocks
 class Conv2d(nn.Module):
     """model_utils.py:27-43."""
@@ -55,7 +77,7 @@ class Conv2d(nn.Module):
         self.activation_fn = activation_fn
 
     def forward(self, x):
-        out = self.conv(x)
+        out = conv1x1(x, self.conv)
         if self.if_bn:
             out = self.bn(out)
         if self.activation_fn is not None:
@@ -234,7 +256,9 @@ class EdgeConv(nn.Module):
             central = torch.zeros(B, C, N, 1, device=inputs.device, dtype=inputs.dtype)
             neigh = inputs.unsqueeze(-1)
         feature = torch.cat((central - neigh, central), dim=1).contiguous(memory_format=torch.channels_last)
-        return max_over_neighbours(self.conv(feature))
+        for m in self.conv:
+            feature = conv1x1(feature, m, "edge") if isinstance(m, nn.Conv2d) else m(feature)
+        return max_over_neighbours(feature)
 
 
 class SinusoidalPositionalEmbedding(nn.Module):
