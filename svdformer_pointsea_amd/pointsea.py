@@ -224,8 +224,9 @@ class Model(nn.Module):
 
     def forward(self, partial, depth):
         partial_cm = partial.transpose(1, 2).contiguous()
-        # the local encoder (EdgeConv kNN, FPS) only depends on the partial cloud:
-        # it runs on a second HIP stream beside the view/point encoder
+        # the local encoder (EdgeConv kNN, FPS, MIOpen convs -- no hipBLASLt GEMMs)
+        # only depends on the partial cloud: it runs on a second HIP stream
+        # beside the view/point encoder
         with fork(partial.device) as br:
             local_feat = self.localencoder(partial_cm)
         feat_g, coarse = self.encoder(partial_cm, depth)

@@ -44,12 +44,16 @@ def max_over_neighbours(x):
 
 import os as _os
 
-# Which 1x1 convs run as GEMMs: "sa" (default) = the SA modules on the main
-# stream.  The local encoder's EdgeConvs run on a side stream (Model.forward)
-# beside hipBLASLt GEMMs of the main stream; hipBLASLt's stream-K kernels
-# synchronise workgroups through a shared workspace, and a graph replay with
-# GEMMs on both streams hung once (PointSea), so the EdgeConvs stay on MIOpen.
-_CONV1X1 = _os.environ.get("PCOPS_CONV1X1", "sa")  # all | edge | sa | off
+# Which 1x1 convs run as GEMMs (A/B switch): sa (default) | all | edge | off.
+# The local encoder's EdgeConvs run on a side stream (Model.forward), and
+# hipBLASLt GEMMs must never run on two streams at once: its stream-K
+# kernels spin-wait on workgroups of the same launch, and two such launches
+# side by side can hold the CUs each other's waiters need (a PointSea graph
+# replay with GEMMs on both streams hung).  So the EdgeConvs stay on MIOpen
+# ("all" measured 68.2 vs 71.3 ms on the PCN step, but is not safe); the
+# side-stream overlap is worth more (local encoder on the main stream with
+# "all": 72.5 ms PCN, 50.9 ms PointSea).
+_CONV1X1 = _os.environ.get("PCOPS_CONV1X1", "sa")
 
 
 def conv1x1(x, conv, where="sa"):
@@ -502,8 +506,9 @@ class Model(nn.Module):
 
     def forward(self, partial, depth):
         partial_cm = partial.transpose(1, 2).contiguous()
-        # the local encoder (EdgeConv kNN, FPS) only depends on the partial cloud:
-        # it runs on a second HIP stream beside the view/point encoder
+        # the local encoder (EdgeConv kNN, FPS, MIOpen convs -- no hipBLASLt GEMMs)
+        # only depends on the partial cloud: it runs on a second HIP stream
+        # beside the view/point encoder
         with fork(partial.device) as br:
             local_feat = self.localencoder(partial_cm)
         feat_g, coarse = self.encoder(partial_cm, depth)
