@@ -64,7 +64,7 @@ def parse():
                     help="PyTorch TunableOp for the dense GEMMs: 'use' the committed per-shape hipBLASLt "
                          "selections in tuning/ (if present), 'tune' them during warm-up (rank 0 "
                          "writes the file), or 'off' (library heuristics)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1_bench_graph_pmc_traffic.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1_final_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
     return ap.parse_args()
