@@ -183,6 +183,14 @@ int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int 
                         const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
                         void *dx16, float *dgamma, float *dbeta, void *workspace, unsigned long long workspace_bytes,
                         pcops_stream_t stream);
+/* pcops_colsum: out[c] = sum_r g[r][c] over a row-major (rows, C) matrix, C % 8 == 0,
+ *   fp32 accumulation in a fixed order (deterministic); g / out dtype codes 0 fp32, 1 bf16.
+ *   Replaces the bias-gradient reduction autograd runs for nn.Linear / 1x1 nn.Conv*d biases
+ *   (torch's g.sum(0) behind F.linear's backward; models/model_utils.py Linear / Conv1d layers).
+ *   workspace: pcops_colsum_workspace_bytes(rows, C). */
+unsigned long long pcops_colsum_workspace_bytes(long long rows, int C);
+int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype, void *workspace,
+                 unsigned long long workspace_bytes, pcops_stream_t stream);
 
 /* ---------------- PCSA spectral gating (models/model_utils.py:358-430) ----------------
  * Per patch p (= b*S + s) of K neighbours x C channels stored [p][k][c] (the

@@ -89,8 +89,23 @@ class _Linear(Function):
         if ctx.needs_input_grad[1]:
             gw = _wgrad(g2.contiguous(), x.reshape(-1, x.shape[-1]).contiguous(), w.dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = g2.sum(0)
+            gb = colsum(g2.contiguous())
         return gx, gw, gb
+
+
+def colsum(g):
+    """g.sum(0) of a (rows, C) CUDA tensor, same dtype: pcops_colsum (fp32 accumulation,
+    deterministic order) when C % 8 == 0, torch's reduction otherwise."""
+    rows, C = g.shape
+    if C % 8 or g.dtype not in _DT or not g.is_contiguous():
+        return g.sum(0)
+    out = torch.empty(C, dtype=g.dtype, device=g.device)
+    wsb = lib().pcops_colsum_workspace_bytes(rows, C)
+    ws = _lib.Workspace.get(g.device, wsb)
+    with torch.cuda.device(g.device):
+        call("colsum", lib().pcops_colsum, ptr(g), _dt(g), rows, C, ptr(out), _DT[g.dtype], ptr(ws), wsb,
+             stream_of(g))
+    return out
 
 
 def linear(x, w, b=None):

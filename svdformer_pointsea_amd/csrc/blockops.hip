@@ -12,6 +12,8 @@
 //                         partial sums in a scratch, then a column reduction
 // dtype codes: 0 = fp32, 1 = bf16.  One wave per row for the LayerNorms
 // (C <= 1024, C % 8 == 0: 16-B vector loads, two-pass statistics in registers).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -149,13 +151,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a,
   }
 }
 
-// Each wave owns kRowsPerWave consecutive rows (one at a time, full row in
-// registers); the block's dgamma / dbeta partial sums are reduced through LDS
-// and written once per block to a [blocks][2C] scratch (plain stores --
-// thousands of waves atomically adding into the same 2C floats serialise),
-// then summed by ln_colsum_kernel.
-constexpr int kRowsPerWave = 4;
-constexpr int kRowsPerBlock = 4 * kRowsPerWave;
+// Each wave owns rpw consecutive rows (one at a time, full row in registers;
+// rpw = 4..16 so that large inputs get ~2048 blocks); the block's dgamma /
+// dbeta partial sums are reduced through LDS (dynamic, 4 x 2C floats) and
+// written once per block to a [blocks][2C] scratch (plain stores -- thousands
+// of waves atomically adding into the same 2C floats serialise), then summed
+// by colsum_final_kernel in a fixed order.
+int ln_bwd_rpw(int rows) {
+  const int r = (rows + 8191) / 8192;
+  return r < 4 ? 4 : (r > 16 ? 16 : r);
+}
 
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g32, const __bf16 *__restrict__ g16,
                                                      const void *__restrict__ a, int adt, const void *__restrict__ b,
@@ -163,8 +168,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
                                                      const float *__restrict__ mean_in,
                                                      const float *__restrict__ rstd_in, int rows, int C,
                                                      float *__restrict__ dx32, __bf16 *__restrict__ dx16,
-                                                     float *__restrict__ part) {
-  __shared__ float red[4][2 * 1024];
+                                                     int rpw, float *__restrict__ part) {
+  extern __shared__ float ln_red[];  // [4][2C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = C >> 3;
   V8 dg[kMaxCh], db[kMaxCh];
@@ -172,8 +177,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
   for (int i = 0; i < kMaxCh; ++i)
 #pragma unroll
     for (int k = 0; k < 8; ++k) dg[i].v[k] = db[i].v[k] = 0.f;
-  const int r0 = blockIdx.x * kRowsPerBlock + w * kRowsPerWave;
-  for (int row = r0; row < r0 + kRowsPerWave && row < rows; ++row) {
+  const int r0 = (blockIdx.x * 4 + w) * rpw;
+  for (int row = r0; row < r0 + rpw && row < rows; ++row) {
     const long long base = (long long)row * C;
     const float mean = mean_in[row], rstd = rstd_in[row];
     V8 xh[kMaxCh], dy[kMaxCh];
@@ -233,48 +238,118 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
     if (ch < nch)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        red[w][8 * ch + k] = dg[i].v[k];
-        red[w][C + 8 * ch + k] = db[i].v[k];
+        ln_red[w * 2 * C + 8 * ch + k] = dg[i].v[k];
+        ln_red[w * 2 * C + C + 8 * ch + k] = db[i].v[k];
       }
   }
   __syncthreads();
   float *pb = part + (long long)blockIdx.x * 2 * C;
-  for (int c = threadIdx.x; c < 2 * C; c += 256) pb[c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+  for (int c = threadIdx.x; c < 2 * C; c += 256)
+    pb[c] = ((ln_red[c] + ln_red[2 * C + c]) + ln_red[4 * C + c]) + ln_red[6 * C + c];
 }
 
-// dgamma / dbeta = column sums of the [blocks][2C] partials, deterministic:
-// grid (2C/64, slices) sums row slices into [slices][2C] (4 waves interleaved
-// over rows), then a (2C/64, 1) launch of the same kernel sums the slices.
-constexpr int kColSlices = 64;
-
-__global__ __launch_bounds__(256) void ln_colsum_kernel(const float *__restrict__ part, int nrows, int C2,
-                                                        float *__restrict__ out, float *__restrict__ dgamma,
-                                                        float *__restrict__ dbeta, int C) {
-  __shared__ float red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int r = threadIdx.x >> 6;
-  const int per = (nrows + gridDim.y - 1) / gridDim.y;
-  const int r0 = blockIdx.y * per, r1 = min(nrows, r0 + per);
-  float s = 0.f;
-  if (col < C2)
-    for (int w = r0 + r; w < r1; w += 4) s += part[(long long)w * C2 + col];
-  red[r][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (r == 0 && col < C2) {
-    const float t = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
-    if (out)
-      out[(long long)blockIdx.y * C2 + col] = t;
-    else if (col < C)
-      dgamma[col] = t;
-    else
-      dbeta[col - C] = t;
-  }
+int ln_bwd_blocks(int rows) {
+  const int rpb = 4 * ln_bwd_rpw(rows);
+  return (rows + rpb - 1) / rpb;
 }
-
-int ln_bwd_blocks(int rows) { return (rows + kRowsPerBlock - 1) / kRowsPerBlock; }
 
 bool dt_ok(int dt) { return dt == 0 || dt == 1; }
 
+// ---------------------------------------------------------------- column sum
+// out[c] = sum_r g[r][c]: the bias gradient of the blocks' Linear / 1x1-conv
+// layers (torch's bf16 sum(0) runs at 0.8-3 TB/s on these (65536, C) inputs).
+// Stage 1: grid (chunks, strips), ~1024 blocks; a wave covers V vector columns
+// (8 elements: one 16-B load for bf16) x 64/V rows per step, 4 waves step
+// through the chunk's rows with up to 16 loads in flight per lane, fp32
+// registers; the chunk's partial row is folded by lane shuffles + LDS and
+// stored once.  Stage 2: 32 columns x 32 chunk groups per block add the
+// <= 1024 partial rows in a fixed order (deterministic, no atomics).
+constexpr int kCsMaxChunks = 1024;
+
+template <int DT>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restrict__ g, long long rows, int C, int V,
+                                                             long long rpc, float *__restrict__ part) {
+  __shared__ float red[4][64 * 8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rw = 64 / V;                         // rows per wave step
+  const int rsub = lane / V, vi = lane - rsub * V;
+  const int col = (blockIdx.y * V + vi) * 8;     // first element column
+  const long long r0 = blockIdx.x * rpc, r1 = min(rows, r0 + rpc);
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const long long step = 4LL * rw;
+  long long r = r0 + w * rw + rsub;
+#pragma unroll 16
+  for (; r < r1; r += step) {
+    V8 t;
+    ld8(t, g, DT, r * C + col);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += t.v[k];
+  }
+  for (int o = V; o < 64; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+  if (rsub == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[w][vi * 8 + k] = acc[k];
+  __syncthreads();
+  const int t = threadIdx.x;
+  for (int i = t; i < V * 8; i += 256) {
+    const float s = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    part[blockIdx.x * (long long)C + blockIdx.y * V * 8 + i] = s;
+  }
+}
+
+// columns [0, split) go to out, [split, C) to out2 (the LayerNorm's dgamma | dbeta)
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float *__restrict__ part, int chunks, int C,
+                                                            void *__restrict__ out, int odt, int split,
+                                                            void *__restrict__ out2) {
+  __shared__ float red[32][33];
+  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + cl;
+  float s = 0.f;
+  if (col < C)
+#pragma unroll 16
+    for (int k = grp; k < chunks; k += 32) s += part[(long long)k * C + col];
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && col < C) {
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) tot += red[i][cl];
+    if (col < split)
+      st(out, odt, col, tot);
+    else
+      st(out2, odt, col - split, tot);
+  }
+}
+
+int colsum_v(int C) {  // vector columns per wave: largest power of two <= 64 dividing C / 8
+  const int nv = C / 8;
+  int V = 64;
+  while (nv % V) V >>= 1;
+  return V;
+}
+
+// tuning knobs (A/B only): PCOPS_COLSUM_BLOCKS (stage-1 blocks aimed at),
+// PCOPS_COLSUM_CHUNKS (cap on partial rows, <= kCsMaxChunks)
+int colsum_env(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+void colsum_shape(long long rows, int C, int &chunks, long long &rpc) {
+  static const int target = colsum_env("PCOPS_COLSUM_BLOCKS", 1024);
+  static const int cap = min(kCsMaxChunks, colsum_env("PCOPS_COLSUM_CHUNKS", kCsMaxChunks));
+  const int strips = C / 8 / colsum_v(C);
+  long long want = (target + strips - 1) / strips;
+  if (want > cap) want = cap;
+  if (want > (rows + 15) / 16) want = (rows + 15) / 16;  // >= 16 rows per chunk
+  if (want < 1) want = 1;
+  rpc = (rows + want - 1) / want;
+  chunks = (int)((rows + rpc - 1) / rpc);
+}
 
 }  // namespace
 
@@ -307,7 +382,7 @@ extern "C" int pcops_layernorm_fwd(const void *a, int a_dtype, const void *b, in
 
 extern "C" unsigned long long pcops_layernorm_bwd_workspace_bytes(int rows, int C) {
   if (rows <= 0 || C <= 0) return 0;
-  return (unsigned long long)(ln_bwd_blocks(rows) + kColSlices) * 2 * C * sizeof(float);
+  return (unsigned long long)ln_bwd_blocks(rows) * 2 * C * sizeof(float);
 }
 
 extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b,
@@ -330,14 +405,45 @@ extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const vo
   if (!workspace || workspace_bytes < pcops_layernorm_bwd_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
   const int blocks = ln_bwd_blocks(rows);
   float *part = (float *)workspace;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 0, s, dy32, (const __bf16 *)dy16, a, a_dtype, b,
-                     b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16, part);
-  float *slice = part + (size_t)blocks * 2 * C;
-  const int slices = blocks < kColSlices ? blocks : kColSlices;
-  hipLaunchKernelGGL(ln_colsum_kernel, dim3((2 * C + 63) / 64, slices), dim3(256), 0, s, part, blocks, 2 * C, slice,
-                     nullptr, nullptr, C);
-  hipLaunchKernelGGL(ln_colsum_kernel, dim3((2 * C + 63) / 64, 1), dim3(256), 0, s, slice, slices, 2 * C, nullptr,
-                     dgamma, dbeta, C);
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 4 * 2 * C * sizeof(float), s, dy32, (const __bf16 *)dy16,
+                     a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16, ln_bwd_rpw(rows), part);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((2 * C + 31) / 32), dim3(1024), 0, s, part, blocks, 2 * C,
+                     (void *)dgamma, 0, C, (void *)dbeta);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" unsigned long long pcops_colsum_workspace_bytes(long long rows, int C) {
+  if (rows <= 0 || C <= 0 || C % 8) return 0;
+  int chunks;
+  long long rpc;
+  colsum_shape(rows, C, chunks, rpc);
+  return (unsigned long long)chunks * C * sizeof(float);
+}
+
+extern "C" int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype,
+                            void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (rows < 0 || C <= 0 || !dt_ok(g_dtype) || !dt_ok(out_dtype) || !out) return PCOPS_ERR_INVALID;
+  if (C % 8) return PCOPS_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  if (rows == 0) {
+    if (hipMemsetAsync(out, 0, (size_t)C * (out_dtype == 0 ? 4 : 2), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!g) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_colsum_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
+  int chunks;
+  long long rpc;
+  colsum_shape(rows, C, chunks, rpc);
+  const int V = colsum_v(C);
+  const dim3 grid(chunks, C / 8 / V);
+  float *part = (float *)workspace;
+  if (g_dtype == 0)
+    hipLaunchKernelGGL(colsum_partial_kernel<0>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, out, out_dtype, C,
+                     nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
