@@ -92,3 +92,17 @@ if os.environ.get("SHAPES"):
         torch.cuda.synchronize()
     print(prof2.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=args.rows,
                                                                max_name_column_width=30, max_shapes_column_width=100))
+
+if os.environ.get("OPS"):
+    # per-shape totals of selected aten ops (e.g. OPS=aten::copy_,aten::add,aten::sum)
+    want = set(os.environ["OPS"].split(","))
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof3:
+        step()
+        torch.cuda.synchronize()
+    rows = []
+    for e in prof3.key_averages(group_by_input_shape=True):
+        if e.key in want:
+            t = getattr(e, "self_device_time_total", 0) or getattr(e, "device_time_total", 0)
+            rows.append((t, e.count, e.key, str(e.input_shapes)[:160]))
+    for t, c, k, s in sorted(rows, reverse=True)[:args.rows]:
+        print(f"{t / 1e3:8.3f} ms {c:4d}x {k:14s} {s}")
