@@ -118,7 +118,7 @@ def synth_55(B, seed, device, n_gt=8192):
 
 
 # ------------------------------------------------------------------ roofline model
-ATTN_ARGS = {"attention forward": 5, "attention bwd dq": 6, "attention bwd dkv": 7}
+ATTN_ARGS = {"attention forward": 5, "attention bwd dq": 7, "attention bwd dkv": 7}  # position of B
 
 
 def kernel_work(name, a):
@@ -127,7 +127,7 @@ def kernel_work(name, a):
     Per-unit figures are SURVEY.md 8(d)'s, restated in DESIGN.md:
       attention fwd   4*BH*Lq*Lk*D FLOP (QK^T + PV)
       attention dkv   8*BH*Lq*Lk*D FLOP (S recompute, dP, dV, dK)
-      attention dq    2*BH*Lq*Lk*D FLOP (dQ only; the S/dP recompute in this
+      attention dq    2*BH*Lq*Lk*D FLOP (dQ only, delta = rowsum(dO*O) fused in; the S/dP recompute in this
                       pass is overhead, not credited -- FA2's 10*BH*Lq*Lk*D
                       total backward count)
       FPS             16 B per point-iteration, B*N*M of them (HBM model)

@@ -153,6 +153,15 @@ int pcops_attention_bwd_dq(const void *q, const void *k, const void *v, const vo
                            long long v_sb, long long v_sh, long long v_srow, long long o_sb, long long o_sh,
                            long long o_srow, const void *workspace, unsigned long long workspace_bytes,
                            pcops_stream_t stream);
+/* preprocess + dQ in one launch (bf16): each query lane forms its delta from the dO
+ * fragment it holds and the matching chunks of o, writes it to workspace for the dK/dV
+ * pass, and computes dQ.  fp32 falls back to the two launches above. */
+int pcops_attention_bwd_dq_delta(const void *q, const void *k, const void *v, const void *o, const void *dout,
+                                 const float *lse, void *dq, int B, int H, int Lq, int Lk, int D, float scale,
+                                 int dtype, long long q_sb, long long q_sh, long long q_srow, long long k_sb,
+                                 long long k_sh, long long k_srow, long long v_sb, long long v_sh, long long v_srow,
+                                 long long o_sb, long long o_sh, long long o_srow, void *workspace,
+                                 unsigned long long workspace_bytes, pcops_stream_t stream);
 int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const void *dout, const float *lse,
                             void *dk, void *dv, int B, int H, int Lq, int Lk, int D, float scale, int dtype,
                             long long q_sb, long long q_sh, long long q_srow, long long k_sb, long long k_sh,

@@ -178,9 +178,8 @@ class AttentionCore(Function):
         qp, kp, vp = _vptr(q_t, qw[1]), _vptr(k_t, kw[1]), _vptr(v_t, vw[1])
         with torch.cuda.device(o.device):
             stream = stream_of(o)
-            call("attention bwd delta", lib().pcops_attention_bwd_preprocess, ptr(o), ptr(do), B, heads, Lq, hd, dt,
-                 ob, hd, orow, ptr(ws), wsb, stream)
-            call("attention bwd dq", lib().pcops_attention_bwd_dq, qp, kp, vp, ptr(do), ptr(lse),
+            # delta = rowsum(dO * O) is formed inside the dQ launch (bf16) and left in ws for dK/dV
+            call("attention bwd dq", lib().pcops_attention_bwd_dq_delta, qp, kp, vp, ptr(o), ptr(do), ptr(lse),
                  _vptr(grads[qw[0]], qw[1]), B, heads, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream)
             call("attention bwd dkv", lib().pcops_attention_bwd_dkv, qp, kp, vp, ptr(do), ptr(lse),
                  _vptr(grads[kw[0]], kw[1]), _vptr(grads[vw[0]], vw[1]), B, heads, Lq, Lk, hd, float(scale), dt,

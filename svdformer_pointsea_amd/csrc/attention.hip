@@ -606,12 +606,18 @@ int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse
 
 // ----------------------------------------------------------------- backward, bf16 (v2)
 // dQ pass: queries on the lane, K/V 64-row tiles double-buffered (as forward).
-template <int D, int NW, int OCC>
+// FD (fused delta): the lane's delta = rowsum(dO * O) is formed from the dO
+// fragment it already holds and the same chunks of O (the two lane halves
+// hold the two halves of the row: one permlane32 swap adds them) and written
+// to delta_out for the dK/dV pass -- no separate preprocess launch, no second
+// read of dO.
+template <int D, int NW, int OCC, bool FD>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dq2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
                                                            const __bf16 *__restrict__ V, const __bf16 *__restrict__ dO,
                                                            const float *__restrict__ lse,
                                                            const float *__restrict__ delta, __bf16 *__restrict__ dQ,
-                                                           int Lq, int Lk, float scale, Strides st) {
+                                                           int Lq, int Lk, float scale, Strides st,
+                                                           const __bf16 *__restrict__ O, float *__restrict__ delta_out) {
   using C = Fwd2Cfg<D, NW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char bwd2_smem[];
   __bf16 *sk = reinterpret_cast<__bf16 *>(bwd2_smem);
@@ -633,7 +639,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
     }
   }
   const float lse2 = qv ? lse[(long long)bh * Lq + qi] * kLog2e : INFINITY;
-  const float dl = qv ? delta[(long long)bh * Lq + qi] : 0.f;
+  float dl;
+  if constexpr (FD) {
+    const __bf16 *orow = O + st.o_off(bh) + (long long)(qv ? qi : 0) * st.o_srow + 8 * h;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const bf16x8 of = qv ? *reinterpret_cast<const bf16x8 *>(orow + 16 * s) : bf16x8{};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part = __builtin_fmaf((float)of[e], (float)gf[s][e], part);
+    }
+    dl = swap_halves_sum(part);
+    if (h == 0 && qv) delta_out[(long long)bh * Lq + qi] = dl;
+  } else {
+    dl = qv ? delta[(long long)bh * Lq + qi] : 0.f;
+  }
   const __bf16 *Kb = K + st.k_off(bh);
   const __bf16 *Vb = V + st.v_off(bh);
   const float sl2 = scale * kLog2e;
@@ -804,20 +824,30 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
   if (MODE != 1) store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
 }
 
-template <int D, int NW>
-int launch_dq2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
-               void *dq, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
+template <int D, int NW, bool FD>
+int launch_dq2_impl(const void *q, const void *k, const void *v, const void *dout, const float *lse,
+                    const float *delta, void *dq, int BH, int Lq, int Lk, float scale, const Strides &st,
+                    const void *o, float *delta_out, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
   constexpr int OCC = (D <= 96 || NW == 8) ? 2 : 1;
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC>,
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC, FD>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
                      (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dq, Lq, Lk,
-                     scale, st);
+                     scale, st, (const __bf16 *)o, delta_out);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
+}
+
+// o == nullptr: delta precomputed (read from `delta`); else fused, written to delta_out
+template <int D, int NW>
+int launch_dq2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+               void *dq, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s,
+               const void *o = nullptr, float *delta_out = nullptr) {
+  return o ? launch_dq2_impl<D, NW, true>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, o, delta_out, s)
+           : launch_dq2_impl<D, NW, false>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, o, delta_out, s);
 }
 
 bool dkv_split() {  // PCOPS_DKV_SPLIT=0 keeps the one-pass dK/dV kernel for D = 128 (A/B runs)
@@ -865,20 +895,21 @@ int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, c
 }
 
 int dq2_dispatch(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
-                 void *dq, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s) {
+                 void *dq, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s,
+                 const void *o = nullptr, float *delta_out = nullptr) {
   const bool wide = Lq > 128;
   switch (D) {
     case 32:
-      return wide ? launch_dq2<32, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s)
-                  : launch_dq2<32, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+      return wide ? launch_dq2<32, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
+                  : launch_dq2<32, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
     case 64:
-      return wide ? launch_dq2<64, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s)
-                  : launch_dq2<64, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+      return wide ? launch_dq2<64, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
+                  : launch_dq2<64, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
     case 96:
-      return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+      return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
     case 128:
-      return wide ? launch_dq2<128, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s)
-                  : launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s);
+      return wide ? launch_dq2<128, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
+                  : launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
     default:
       return PCOPS_ERR_UNSUPPORTED;
   }
@@ -1092,6 +1123,33 @@ extern "C" int pcops_attention_bwd_dq(const void *q, const void *k, const void *
   return dq2_dispatch(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, D, scale, st, s);
 }
 
+extern "C" int pcops_attention_bwd_dq_delta(const void *q, const void *k, const void *v, const void *o,
+                                            const void *dout, const float *lse, void *dq, int B, int H, int Lq, int Lk,
+                                            int D, float scale, int dtype, PC_ATTN_STRIDES, void *workspace,
+                                            unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (B < 0 || H <= 0) return PCOPS_ERR_INVALID;
+  int rc = check_common(B * H, Lq, Lk, D, dtype);
+  if (rc) return rc;
+  const int BH = B * H;
+  if (BH == 0 || Lq == 0) return PCOPS_OK;
+  if (dtype == 0 || use_v1()) {  // fp32 / first-generation kernels: the two-launch form
+    rc = pcops_attention_bwd_preprocess(o, dout, B, H, Lq, D, dtype, o_sb, o_sh, o_srow, workspace, workspace_bytes,
+                                        stream);
+    if (rc) return rc;
+    return pcops_attention_bwd_dq(q, k, v, dout, lse, dq, B, H, Lq, Lk, D, scale, dtype, PC_ATTN_STRIDE_ARGS,
+                                  workspace, workspace_bytes, stream);
+  }
+  if (!q || !k || !v || !o || !dout || !lse || !dq || Lk <= 0) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_workspace_bytes(B, H, Lq, Lk, D)) return PCOPS_ERR_WORKSPACE;
+  if (!aligned_ok(q, q_sb, q_sh, q_srow, 2) || !aligned_ok(k, k_sb, k_sh, k_srow, 2) ||
+      !aligned_ok(v, v_sb, v_sh, v_srow, 2) || !aligned_ok(dout, o_sb, o_sh, o_srow, 2) ||
+      !aligned_ok(o, o_sb, o_sh, o_srow, 2) || !aligned_ok(dq, q_sb, q_sh, q_srow, 2))
+    return PCOPS_ERR_UNSUPPORTED;
+  const Strides st{PC_ATTN_STRIDE_ARGS, H};
+  return dq2_dispatch(q, k, v, dout, lse, nullptr, dq, BH, Lq, Lk, D, scale, st, (hipStream_t)stream, o,
+                      (float *)workspace);
+}
+
 extern "C" int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const void *dout,
                                        const float *lse, void *dk, void *dv, int B, int H, int Lq, int Lk, int D,
                                        float scale, int dtype, PC_ATTN_STRIDES, const void *workspace,
@@ -1125,11 +1183,8 @@ extern "C" int pcops_attention_backward(const void *q, const void *k, const void
   if (B == 0 || Lq == 0 || Lk == 0) return check_common(B * H, Lq, Lk, D, dtype);
   const int es = dtype == 0 ? 4 : 2;
   if (o && !aligned_ok(o, o_sb, o_sh, o_srow, es)) return PCOPS_ERR_UNSUPPORTED;
-  int rc = pcops_attention_bwd_preprocess(o, dout, B, H, Lq, D, dtype, o_sb, o_sh, o_srow, workspace, workspace_bytes,
-                                          stream);
-  if (rc) return rc;
-  rc = pcops_attention_bwd_dq(q, k, v, dout, lse, dq, B, H, Lq, Lk, D, scale, dtype, PC_ATTN_STRIDE_ARGS, workspace,
-                              workspace_bytes, stream);
+  int rc = pcops_attention_bwd_dq_delta(q, k, v, o, dout, lse, dq, B, H, Lq, Lk, D, scale, dtype, PC_ATTN_STRIDE_ARGS,
+                                        workspace, workspace_bytes, stream);
   if (rc) return rc;
   return pcops_attention_bwd_dkv(q, k, v, dout, lse, dk, dv, B, H, Lq, Lk, D, scale, dtype, PC_ATTN_STRIDE_ARGS,
                                  workspace, workspace_bytes, stream);
