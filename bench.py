@@ -391,7 +391,8 @@ def main():
     # weights refreshed by one cast per step (svdformer_pointsea_amd/train.py)
     fp = FlatParams(model, device, bf16=amp)
     use_graph = not args.no_graph
-    opt = wl.optimizer(model.parameters(), fused=True, capturable=use_graph)
+    # one parameter group, elementwise update: Adam over the flat master buffer
+    opt = wl.optimizer([fp.master()], fused=True, capturable=use_graph)
     partial, gt = wl.synth(args.batch, 1000 + rank, device)
     # ShapeNet-55 re-crops its partial input from gt inside the step; the crop
     # draws come from the device's default generator (graph-capturable)

@@ -40,3 +40,24 @@ def test_flat_params_match_autocast_grads():
         assert torch.equal(pa.data, pb.data), n
     # the fp32 master weights are the parameters themselves (views of one buffer)
     assert all(p.data_ptr() >= fp.flat.data_ptr() for p in b.parameters())
+
+
+def test_flat_master_optimizer_equals_per_tensor():
+    """Adam / AdamW over FlatParams.master() (one tensor) == per-tensor updates."""
+    for make in (lambda ps: torch.optim.Adam(ps, lr=1e-2, betas=(0.9, 0.999)),
+                 lambda ps: torch.optim.AdamW(ps, lr=1e-2, weight_decay=5e-4)):
+        torch.manual_seed(1)
+        a = _Net()
+        b = copy.deepcopy(a)
+        fa, fb = FlatParams(a, "cpu", bf16=False), FlatParams(b, "cpu", bf16=False)
+        oa, ob = make(list(a.parameters())), make([fb.master()])
+        for step in range(3):
+            x = torch.randn(3, 8, 5, generator=torch.Generator().manual_seed(step))
+            for f in (fa, fb):
+                f.zero_grad()
+                f.forward(x).backward()
+            oa.step()
+            ob.step()
+        assert torch.equal(fa.flat, fb.flat)
+        for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+            assert torch.equal(pa.data, pb.data), n

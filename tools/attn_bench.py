@@ -35,6 +35,8 @@ for si, (Lq, Lk, E, H) in enumerate(shapes):
     out = []
     for name, mult in [("attention forward", 1), ("attention bwd dq", 0.5), ("attention bwd dkv", 2.0),
                        ("attention bwd delta", 0)]:
+        if name not in summ:   # delta is fused into the dq launch (bf16)
+            continue
         n, mean, tot = summ[name]
         tf = fl * mult / (mean * 1e-3) / 1e12 if mult else 0
         out.append(f"{name.split()[-1]} {mean:.3f}ms {tf:.0f}TF")
