@@ -13,16 +13,26 @@ FlatParams keeps the same numerics with three flat buffers instead:
     weights and biases) come first, and their bf16 shadows are views of a
     flat bf16 buffer, refreshed by ONE cast kernel per step;
   * the model runs through torch.func.functional_call on the bf16 shadows, so
-    autocast finds bf16 operands and casts nothing; their gradients land in a
-    flat bf16 buffer and go back into the fp32 bucket with ONE cast kernel.
+    autocast finds bf16 operands and casts nothing; autograd hands each shadow
+    its gradient tensor (no pre-set .grad, so no accumulate-add per use: ~200
+    tiny add kernels per PCN step), and collect() concatenates them in bucket
+    order into a flat bf16 buffer and widens that into the fp32 bucket (a few
+    batched-copy launches + ONE cast kernel).
 Values are unchanged: under autocast those GEMMs/convs already read the
 bf16-rounded weights and produce bf16 weight gradients that are then
 widened, which is exactly what the two flat casts do.  Parameters outside
 the eligible set (LayerNorm, BatchNorm) stay fp32 and get fp32 gradients
 directly in the bucket.
 """
+import os
+
 import torch
 from torch import nn
+
+# A/B switch: "cat" (default) lets autograd own the shadows' gradients;
+# "preset" pre-assigns them as views of the flat bf16 buffer (autograd then
+# accumulates into them with one add kernel per use)
+_GRADS = os.environ.get("PCOPS_FLATGRAD", "cat")
 
 _ELIGIBLE = (nn.Linear, nn.Conv1d, nn.Conv2d, nn.ConvTranspose1d)
 
@@ -49,6 +59,7 @@ class FlatParams:
         self.flat16 = torch.empty(self.n16, dtype=torch.bfloat16, device=device)
         self.grad16 = torch.zeros(self.n16, dtype=torch.bfloat16, device=device)
         self.shadow = {}
+        self._order = []   # bf16-eligible shadows in bucket order
         off = 0
         with torch.no_grad():
             for name, p in named:
@@ -60,8 +71,10 @@ class FlatParams:
                 if name in low:
                     w = self.flat16[off:off + n].as_strided(p.shape, p.stride())
                     w.requires_grad_(True)
-                    w.grad = self.grad16[off:off + n].as_strided(p.shape, p.stride())
+                    if _GRADS == "preset":
+                        w.grad = self.grad16[off:off + n].as_strided(p.shape, p.stride())
                     self.shadow[name] = w
+                    self._order.append(w)
                 off += n
 
     def master(self):
@@ -77,7 +90,11 @@ class FlatParams:
 
     def zero_grad(self):
         self.grad[self.n16:].zero_()   # grad[:n16] is overwritten by collect()
-        self.grad16.zero_()
+        if _GRADS == "preset":
+            self.grad16.zero_()
+            return
+        for w in self._order:
+            w.grad = None
 
     def refresh(self):
         """bf16 shadows <- fp32 master weights (one cast kernel)."""
@@ -90,9 +107,30 @@ class FlatParams:
             return self.model(*args, **kwargs)
         return torch.func.functional_call(self.model, self.shadow, args, kwargs, strict=False)
 
+    @staticmethod
+    def _physical(g, w):
+        """g's elements in w's memory order, as a 1-D tensor (w is a dense view)."""
+        if g.stride() != w.stride():
+            h = torch.empty_strided(w.shape, w.stride(), dtype=g.dtype, device=g.device)
+            h.copy_(g)
+            g = h
+        return g.as_strided((g.numel(),), (1,), g.storage_offset())
+
     def collect(self):
-        """fp32 gradient bucket <- the shadows' bf16 gradients (one cast kernel)."""
+        """fp32 gradient bucket <- the shadows' bf16 gradients (zeros where a
+        shadow received none): one batched concatenation, one cast kernel."""
+        if not self._order:
+            return
         with torch.no_grad():
+            if _GRADS == "preset":
+                self.grad[:self.n16].copy_(self.grad16)
+                return
+            parts = []
+            for w in self._order:
+                g = w.grad
+                parts.append(torch.zeros(w.numel(), dtype=self.grad16.dtype, device=self.grad16.device)
+                             if g is None else self._physical(g, w))
+            torch.cat(parts, out=self.grad16)
             self.grad[:self.n16].copy_(self.grad16)
 
     def allreduce(self, world):

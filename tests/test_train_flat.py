@@ -61,3 +61,37 @@ def test_flat_master_optimizer_equals_per_tensor():
         assert torch.equal(fa.flat, fb.flat)
         for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
             assert torch.equal(pa.data, pb.data), n
+
+
+class _Net2(nn.Module):
+    """A Linear used twice, a Linear never used, a channels_last Conv2d."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(4, 6, 1).to(memory_format=torch.channels_last)
+        self.lin = nn.Linear(6, 6)
+        self.unused = nn.Linear(3, 3)
+
+    def forward(self, x):
+        y = self.conv(x.contiguous(memory_format=torch.channels_last)).flatten(2).transpose(1, 2)
+        return self.lin(torch.relu(self.lin(y))).float().square().mean()
+
+
+def test_flat_params_reused_unused_and_channels_last():
+    torch.manual_seed(3)
+    a = _Net2()
+    b = copy.deepcopy(a)
+    x = torch.randn(2, 4, 3, 5)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        a(x).backward()
+    fp = FlatParams(b, "cpu")
+    assert b.conv.weight.is_contiguous(memory_format=torch.channels_last)
+    for _ in range(2):   # the second step must not accumulate into the first
+        fp.zero_grad()
+        fp.refresh()
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            fp.forward(x).backward()
+        fp.collect()
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        ref = torch.zeros_like(pa) if pa.grad is None else pa.grad
+        assert torch.equal(ref, pb.grad), n
