@@ -21,6 +21,7 @@ flash-style MFMA kernel: fp32 (exact f32 MFMA, the parity build) or bf16
 (fp32 accumulate) following the dtype of its inputs (e.g. torch.autocast).
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -408,6 +409,35 @@ class _BlockBase(nn.Module):
         return layer_norm(self.norm13, y)
 
 
+class _AddToBf16(Function):
+    """bf16(a + b) in one kernel for a block output that only feeds GEMMs:
+    the same value autocast would produce from the fp32 sum (one rounding),
+    without materialising the fp32 sum; backward casts the bf16 gradient once
+    (a's dtype) instead of widening it and narrowing it again."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        out = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
+        torch.add(a, b, out=out)
+        ctx.dts = (a.dtype, b.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dts[0]), g.to(ctx.dts[1])
+
+
+def block_sum(s, f):
+    """s + f of a block's (residual, FFN) outputs whose consumers are GEMMs
+    (input_proj / conv_ps): bf16 directly under bf16 autocast, else s + f."""
+    if _BLOCK_SUM16 and _want_bf16() and s.is_cuda:
+        return _AddToBf16.apply(s, f)
+    return s + f
+
+
+_BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
+
+
 def _pos_tokens(pos):
     # the reference passes pos seq-first (L, B, C)
     return None if pos is None else pos.transpose(0, 1)
@@ -472,8 +502,8 @@ class SDG_Decoder(nn.Module):
 
     def forward_tokens(self, x_tok):
         s, f = self.sa1.forward_tokens(x_tok)
-        s, f = self.sa2.forward_tokens(s + f)
-        return s + f
+        s, f = self.sa2.forward_tokens(block_sum(s, f))   # sa2 starts with input_proj (a GEMM)
+        return block_sum(s, f)                             # SDG feeds it to input_proj / conv_ps
 
     def forward(self, input):
         s, f = self.sa1.forward_tokens(to_tokens(input))

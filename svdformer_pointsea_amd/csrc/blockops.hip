@@ -162,6 +162,7 @@ int ln_bwd_rpw(int rows) {
   return r < 4 ? 4 : (r > 16 ? 16 : r);
 }
 
+template <int CH>  // 8-element chunks per lane: 1 for C <= 512 (half the registers), 2 for C <= 1024
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g32, const __bf16 *__restrict__ g16,
                                                      const void *__restrict__ a, int adt, const void *__restrict__ b,
                                                      int bdt, const float *__restrict__ gamma,
@@ -172,19 +173,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
   extern __shared__ float ln_red[];  // [4][2C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = C >> 3;
-  V8 dg[kMaxCh], db[kMaxCh];
+  V8 dg[CH], db[CH];
 #pragma unroll
-  for (int i = 0; i < kMaxCh; ++i)
+  for (int i = 0; i < CH; ++i)
 #pragma unroll
     for (int k = 0; k < 8; ++k) dg[i].v[k] = db[i].v[k] = 0.f;
   const int r0 = (blockIdx.x * 4 + w) * rpw;
   for (int row = r0; row < r0 + rpw && row < rows; ++row) {
     const long long base = (long long)row * C;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    V8 xh[kMaxCh], dy[kMaxCh];
+    V8 xh[CH], dy[CH];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxCh; ++i) {
+    for (int i = 0; i < CH; ++i) {
       const int ch = lane + 64 * i;
       if (ch < nch) {
         V8 t;
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
     const float mg = wave_sum_f32(sg) / (float)C;
     const float mgx = wave_sum_f32(sgx) / (float)C;
 #pragma unroll
-    for (int i = 0; i < kMaxCh; ++i) {
+    for (int i = 0; i < CH; ++i) {
       const int ch = lane + 64 * i;
       if (ch < nch) {
         V8 dx;
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
     }
   }
 #pragma unroll
-  for (int i = 0; i < kMaxCh; ++i) {
+  for (int i = 0; i < CH; ++i) {
     const int ch = lane + 64 * i;
     if (ch < nch)
 #pragma unroll
@@ -405,8 +406,18 @@ extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const vo
   if (!workspace || workspace_bytes < pcops_layernorm_bwd_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
   const int blocks = ln_bwd_blocks(rows);
   float *part = (float *)workspace;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(blocks), dim3(256), 4 * 2 * C * sizeof(float), s, dy32, (const __bf16 *)dy16,
-                     a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16, ln_bwd_rpw(rows), part);
+  static const bool force2 = [] {  // A/B: PCOPS_LN_CH2=1 runs every C on the two-chunk kernel
+    const char *e = getenv("PCOPS_LN_CH2");
+    return e && e[0] == '1';
+  }();
+  if (C <= 512 && !force2)
+    hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 4 * 2 * C * sizeof(float), s, dy32,
+                       (const __bf16 *)dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16,
+                       ln_bwd_rpw(rows), part);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 4 * 2 * C * sizeof(float), s, dy32,
+                       (const __bf16 *)dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16,
+                       ln_bwd_rpw(rows), part);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((2 * C + 31) / 32), dim3(1024), 0, s, part, blocks, 2 * C,
                      (void *)dgamma, 0, C, (void *)dbeta);
   PC_CHECK_LAUNCH();

@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import SDG_Decoder, cross_attention, linear, self_attention, to_channels, to_tokens
+from .attention import SDG_Decoder, block_sum, cross_attention, linear, self_attention, to_channels, to_tokens
 from .chamfer3D import chamfer_3DDist
 from .model_utils import fps_subsample, group_local, sample_and_group_knn
 from ._lib import fork
@@ -395,7 +395,7 @@ class SDG(nn.Module):
         if isinstance(dec, SDG_Decoder):
             return dec.forward_tokens(x)
         s, f = dec.forward_tokens(x)
-        return s + f
+        return block_sum(s, f)
 
     def forward_tokens(self, local_tok, coarse, f_g, partial):
         """Token-major SDG: local_tok (B,512,C), coarse (B,N,3), f_g (B,512,1),
@@ -411,12 +411,12 @@ class SDG(nn.Module):
         # (B,N,hidden).reshape(B,hidden,N).permute(2,0,1) of the reference, token-major
         pos = self.embedding(half_cd).reshape(B, self.hidden, N).transpose(1, 2)
         s, f = self.sa1.forward_tokens(F_, pos)
-        F_Q = s + f
+        F_Q = block_sum(s, f)   # feeds decoder1 / cross1, both starting with input_proj
         F_Q_ = self._decode(self.decoder1, F_Q)
         # similarity alignment with the local features
         local = _lin(self.mlpp.mlp[2], self.mlpp.mlp[1](_lin(self.mlpp.mlp[0], local_tok)))
         s, f = self.cross1.forward_tokens(F_Q, local)
-        F_H_ = self._decode(self.decoder2, s + f)
+        F_H_ = self._decode(self.decoder2, block_sum(s, f))
         T = _lin(self.conv_ps, torch.cat([F_Q_.to(F_H_.dtype), F_H_], dim=-1))
         # (B, C*r, N).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n
         r = self.ratio
