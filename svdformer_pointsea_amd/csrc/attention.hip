@@ -373,6 +373,10 @@ __global__ __launch_bounds__(kThreads) void attn_dkv_kernel(const T *__restrict_
 // is on the matrix cores; one barrier per tile.  Half-wave exchange by
 // v_permlane32_swap; the softmax scale folded into the exp2 argument (fma).
 constexpr int kKT = 64;  // keys per tile
+#ifndef PCOPS_DEFER_LOG2
+#define PCOPS_DEFER_LOG2 8.f  // 0 = rescale on every max increase (A/B builds)
+#endif
+constexpr float kDeferLog2 = PCOPS_DEFER_LOG2;  // forward: rescale only when a row max grows by > 2^8
 
 __device__ __forceinline__ float swap_halves_max(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -565,8 +569,13 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
 #pragma unroll
     for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(X0[r], X1[r]));
     tmax = swap_halves_max(tmax);
-    const float mn = fmaxf(m, tmax * sl2);
-    const float alpha = exp2f(m - mn);
+    // deferred max (guide T13): while no row's tile max exceeds its running
+    // max by more than kDeferLog2 (P <= 2^8), keep m and skip the O rescale;
+    // the decision is wave-uniform and taken before this tile's P exists
+    const float pm = tmax * sl2;
+    const bool keep = __all(pm - m <= kDeferLog2);
+    const float mn = keep ? m : fmaxf(m, pm);
+    const float alpha = keep ? 1.f : exp2f(m - mn);
     float rs = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -577,7 +586,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     rs = swap_halves_sum(rs);
     lsum = lsum * alpha + rs;
     m = mn;
-    if (alpha != 1.f) {
+    if (!keep) {
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) Y[db] *= alpha;
     }

@@ -288,3 +288,27 @@ def test_colsum_matches_float64(dev, rows, C, dtype):
     atol = 1e-5 * max(1, rows) ** 0.5 + (2 ** -7 * ref.abs() if dtype == torch.bfloat16 else 0)
     err = (out.cpu().double() - ref).abs()
     assert bool((err <= atol + 1e-4 * ref.abs()).all()), err.max()
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+def test_core_bf16_growing_row_max(dev, hd):
+    """Scores that grow along the keys at a per-row rate, so row maxima rise
+    by 0.3..20 (log2 units) per 64-key tile: the forward's deferred-rescale
+    branch (keep the running max while growth <= 2^8) and the rescale branch
+    both fire, with mixed lanes in one wave.  bf16 inputs, float64 reference."""
+    from svdformer_pointsea_amd.attention import attention_core
+
+    B, H, Lq, Lk = 2, 2, 96, 640
+    E = H * hd
+    g = torch.Generator().manual_seed(hd)
+    rate = torch.rand(Lq, B, H, 1, generator=g) * 1.2 + 0.02          # per (query, head) growth
+    q = torch.randn(Lq, B, H, hd, generator=g) * 0.1
+    q[..., 0] = rate[..., 0] * math.sqrt(hd)                           # score ~ rate * key_position
+    k = torch.randn(Lk, B, H, hd, generator=g) * 0.1
+    k[..., 0] = torch.arange(Lk, dtype=torch.float32).view(Lk, 1, 1) / 64.0 * 8.0
+    v = torch.rand(Lk, B, H, hd, generator=g) * 2 - 1
+    qb, kb, vb = [t.reshape(t.shape[0], B, E).to(dev, torch.bfloat16) for t in (q, k, v)]
+    o = attention_core(qb, kb, vb, H)
+    ref = _ref(qb.float(), kb.float(), vb.float(), H)
+    err = (o.double() - ref).abs().max().item()
+    assert err < 2e-2, err
