@@ -424,7 +424,8 @@ class _AddToBf16(Function):
 
     @staticmethod
     def backward(ctx, g):
-        return g.to(ctx.dts[0]), g.to(ctx.dts[1])
+        ga = g.to(ctx.dts[0])
+        return ga, (ga if ctx.dts[1] == ctx.dts[0] else g.to(ctx.dts[1]))
 
 
 def block_sum(s, f):
@@ -455,7 +456,7 @@ class self_attention(_BlockBase):
         if pos is None:
             attn = self.multihead_attn(s1h, s1h, s1h)[0]
         else:
-            q = s1 + pos
+            q = block_sum(s1, pos)   # only the q/k projection GEMM reads it
             attn = self.multihead_attn(q, q, s1h)[0]
         return self._tail(s1, attn)
 
@@ -471,9 +472,11 @@ class cross_attention(_BlockBase):
         super().__init__(d_model, d_model_out, nhead, dim_feedforward, dropout)
 
     def forward_tokens(self, x1_tok, x2_tok, pos=None):
-        s1, _ = self._in(x1_tok)
+        s1, s1h = self._in(x1_tok)
         _, s2h = self._in(x2_tok)
-        q = self.with_pos_embed(s1, pos)
+        # the query only feeds its projection GEMM: the LN's bf16 copy is
+        # exactly what autocast would cast s1 to
+        q = s1h if pos is None else block_sum(s1, pos)
         attn = self.multihead_attn(q, s2h, s2h)[0]
         return self._tail(s1, attn)
 
