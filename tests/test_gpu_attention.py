@@ -20,6 +20,8 @@ SHAPES = [  # (B, H, Lq, Lk, E)
     (1, 8, 2048, 512, 512), # refine2 cross
     (1, 8, 333, 250, 1024), # ragged hd 128 (split dK/dV path)
     (2, 2, 70, 130, 64),    # hd 32
+    (2, 8, 2048, 2048, 512),   # refine2 self-attention at its real length (hd 64, 32 key tiles)
+    (2, 8, 2048, 2048, 1024),  # refine2 decoder sa2 at its real length (hd 128)
 ]
 
 
@@ -312,3 +314,81 @@ def test_core_bf16_growing_row_max(dev, hd):
     ref = _ref(qb.float(), kb.float(), vb.float(), H)
     err = (o.double() - ref).abs().max().item()
     assert err < 2e-2, err
+    # the log-sum-exp the forward leaves for both backward passes, built from a
+    # row max that the deferral may have kept stale: exact math says it must
+    # still equal logsumexp(scale * q k^T) per (batch*head, query)
+    lse = _forward_lse(qb, kb, vb, H)
+    s = torch.einsum("qbhd,kbhd->bhqk", qb.float().double().reshape(Lq, B, H, hd),
+                     kb.float().double().reshape(Lk, B, H, hd)) / math.sqrt(hd)
+    ref_lse = torch.logsumexp(s, -1).reshape(B * H, Lq)
+    assert (lse.double() - ref_lse).abs().max().item() < 1e-3
+    # and the gradients that read it (dQ, dK, dV) against float64 autograd
+    gq = torch.randn(Lq, B, E, generator=torch.Generator().manual_seed(7)).to(dev)
+    qs, ks, vs = [t.detach().clone().requires_grad_(True) for t in (qb, kb, vb)]
+    (attention_core(qs, ks, vs, H).float() * gq).sum().backward()
+    qd, kd, vd = [t.detach().double().clone().requires_grad_(True) for t in (qb, kb, vb)]
+    (_ref(qd, kd, vd, H) * gq.double()).sum().backward()
+    for a, b in [(qs.grad, qd.grad), (ks.grad, kd.grad), (vs.grad, vd.grad)]:
+        rel = (a.double() - b).norm().item() / max(b.norm().item(), 1e-6)
+        assert rel < 3e-2, rel
+
+
+def _forward_lse(q, k, v, H):
+    """Call pcops_attention_forward directly and return its (B*H, Lq) log-sum-exp."""
+    from svdformer_pointsea_amd import _lib
+    from svdformer_pointsea_amd._lib import lib, ptr, stream_of
+
+    Lq, B, E = q.shape
+    Lk, hd = k.shape[0], E // H
+    o = torch.empty_like(q)
+    lse = torch.empty(B * H, Lq, dtype=torch.float32, device=q.device)
+    dt = 1 if q.dtype == torch.bfloat16 else 0
+    st = (q.stride(1), hd, q.stride(0), k.stride(1), hd, k.stride(0), v.stride(1), hd, v.stride(0),
+          o.stride(1), hd, o.stride(0))
+    _lib.call("attention forward", lib().pcops_attention_forward, ptr(q), ptr(k), ptr(v), ptr(o), ptr(lse), B, H,
+              Lq, Lk, hd, 1.0 / math.sqrt(hd), dt, *st, stream_of(q))
+    torch.cuda.synchronize()
+    return lse
+
+
+def _large_case(name):
+    import sys
+
+    from conftest import GOLDEN
+
+    sys.path.insert(0, GOLDEN)
+    from make_golden_attn_large import CASES, inputs
+
+    return CASES[name], inputs(CASES[name])
+
+
+@pytest.mark.parametrize("name", ["sa2048", "ca2048x512", "dec2048", "sa512"])
+def test_blocks_large_golden(dev, name):
+    """Blocks at the PCN step's real lengths (L = 2048 self, 2048 x 512 cross,
+    hd 64 / 96 / 128) against the reference's own modules
+    (tests/golden/make_golden_attn_large.py): 1e-5 abs on every kept output,
+    the per-channel / per-token sums within 1e-5 per summed element."""
+    import sys
+
+    from conftest import GOLDEN
+
+    sys.path.insert(0, GOLDEN)
+    from weights import fill_state
+
+    from svdformer_pointsea_amd import attention as A
+
+    c, args = _large_case(name)
+    if c["kind"] == "self":
+        m = A.self_attention(c["cin"], c["cout"], nhead=8)
+    elif c["kind"] == "cross":
+        m = A.cross_attention(c["cin"], c["cout"], nhead=8)
+    else:
+        m = A.SDG_Decoder(c["cin"], c["cout"], c["ratio"])
+    m = fill_state(m, seed=c["wseed"]).eval().to(dev)
+    g = golden("attention_large.npz")
+    with torch.no_grad():
+        y = m(*[a.to(dev) for a in args]).cpu()
+    np.testing.assert_allclose(y[..., :128].numpy(), g[f"{name}_cols"], rtol=0, atol=1e-5)
+    L, C = y.shape[2], y.shape[1]
+    np.testing.assert_allclose(y.double().sum(2).numpy(), g[f"{name}_csum"], rtol=0, atol=1e-5 * L)
+    np.testing.assert_allclose(y.double().sum(1).numpy(), g[f"{name}_tsum"], rtol=0, atol=1e-5 * C)

@@ -1,0 +1,57 @@
+#!/bin/bash
+# One parameterised GPU session (replaces the round-1 one-off gpu_round_s*.sh):
+#   bash tools/gpu_run.sh <out-dir> <stage> [<stage> ...]
+# Stages (each under its own time limit; the chain stops at the first failure):
+#   tests        pytest -m gpu (thread timeouts, names a hung test)
+#   smoke        __graft_entry__.smoke()
+#   probe        tools/valu_probe (VALU issue cost per instruction kind)
+#   bench        bench.py default line (PCN, N=1)
+#   bench_ps     bench.py --model pointsea
+#   bench_fp32   bench.py --fp32 --batch 16 (configs[1] numerics)
+#   trace        rocprofv3 --kernel-trace --stats of bench.py
+#   pmc_traffic  two PMC passes (FETCH_SIZE / WRITE_SIZE) -> tools/pmc_traffic.py
+#   pmc_attn     SQ counter pass over the attention kernels (tools/attn_bench.py)
+#   avail        rocprofv3 --list-avail
+#   knn          tools/knn_bench.py ; chamfer: tools/microbench.py chamfer
+set -o pipefail
+OUT=${1:?out dir}; shift
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PMC_RE='attn_|ln_|fps_|chamfer_|knn|colsum|pcsa|gather|group|depth|points2|grid2|transpose_add'
+run_stage() {
+  case "$1" in
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+             > "$OUT/pytest_gpu.log" 2>&1 ;;
+    smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$OUT/smoke.log" 2>&1 ;;
+    probe) timeout -k 10 60 ./tools/valu_probe > "$OUT/valu_probe.txt" 2>&1 ;;
+    bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    bench_ps) timeout -k 10 500 python bench.py --model pointsea > "$OUT/bench_pointsea.json" 2> "$OUT/bench_pointsea.err" ;;
+    bench_fp32) timeout -k 10 500 python bench.py --fp32 --batch 16 --no-cpu-baseline > "$OUT/bench_fp32.json" \
+                  2> "$OUT/bench_fp32.err" ;;
+    trace) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+             python bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_traced.json" 2> "$OUT/trace.err" ;;
+    pmc_traffic)
+      timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
+        -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+        > /dev/null 2> "$OUT/pmc_fetch.err" &&
+      timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
+        -d "$OUT/pmc_write" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+        > /dev/null 2> "$OUT/pmc_write.err" &&
+      python tools/pmc_traffic.py "$(find "$OUT/pmc_fetch" -name '*counter_collection.csv' -print -quit)" \
+        "$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)" "$OUT/pmc_traffic.json" ;;
+    pmc_attn)
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA \
+        SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+        --kernel-include-regex 'attn_' --output-format csv -d "$OUT/pmc_attn" -o run -- \
+        python tools/attn_bench.py 0 1 > "$OUT/pmc_attn.log" 2>&1 ;;
+    avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
+    knn) timeout -k 10 120 python tools/knn_bench.py > "$OUT/knn_bench.txt" 2>&1 ;;
+    chamfer) timeout -k 10 120 python tools/microbench.py > "$OUT/chamfer_bench.txt" 2>&1 ;;
+    *) echo "unknown stage $1"; return 2 ;;
+  esac
+}
+for s in "$@"; do
+  echo "[gpu_run $(date +%T)] $s"
+  run_stage "$s" || { rc=$?; echo "[gpu_run] stage $s failed rc=$rc"; exit $rc; }
+  echo "[gpu_run $(date +%T)] $s ok"
+done

@@ -8,8 +8,10 @@ template <int KIND>
 __global__ __launch_bounds__(1024) void k(float *out, unsigned long long *cyc, int iters) {
   float a[CHAINS], b = 1.0001f + threadIdx.x * 1e-7f, c = 0.999f;
   int ia[CHAINS];
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 p[CHAINS], pb = {b, b * 1.0001f}, pc = {c, c};
 #pragma unroll
-  for (int i = 0; i < CHAINS; ++i) { a[i] = threadIdx.x * 1e-3f + i; ia[i] = threadIdx.x + i; }
+  for (int i = 0; i < CHAINS; ++i) { a[i] = threadIdx.x * 1e-3f + i; ia[i] = threadIdx.x + i; p[i] = f2{a[i], a[i] + 0.5f}; }
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
@@ -19,13 +21,16 @@ __global__ __launch_bounds__(1024) void k(float *out, unsigned long long *cyc, i
       if (KIND == 2) ia[i] = min(ia[i] ^ 0x55, (int)it);                 // v_xor + v_min_i32
       if (KIND == 3) ia[i] = ia[i] + it;                                 // v_add_u32
       if (KIND == 4) a[i] = fmaxf(a[i] * b, c);                          // v_mul + v_max
+      if (KIND == 5) p[i] = __builtin_elementwise_fma(p[i], pb, pc);     // v_pk_fma_f32
+      if (KIND == 6) p[i] = p[i] - pb;                                   // v_pk_add_f32
+      if (KIND == 7) p[i] = p[i] * pb;                                   // v_pk_mul_f32
     }
     asm volatile("" ::: "memory");
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
   float s = 0; int si = 0;
 #pragma unroll
-  for (int i = 0; i < CHAINS; ++i) { s += a[i]; si += ia[i]; }
+  for (int i = 0; i < CHAINS; ++i) { s += a[i] + p[i].x + p[i].y; si += ia[i]; }
   out[blockIdx.x * blockDim.x + threadIdx.x] = s + si;
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
@@ -53,5 +58,8 @@ int main() {
   run<2>("v_xor+v_min_i32", 2, out, cyc);
   run<3>("v_add_u32", 1, out, cyc);
   run<4>("v_mul_f32+v_max_f32", 2, out, cyc);
+  run<5>("v_pk_fma_f32", 1, out, cyc);
+  run<6>("v_pk_add_f32", 1, out, cyc);
+  run<7>("v_pk_mul_f32", 1, out, cyc);
   return 0;
 }
