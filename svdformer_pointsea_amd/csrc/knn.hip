@@ -135,16 +135,69 @@ __device__ __forceinline__ void merge_and_store(MergeBuf<KK, G> &mb, const float
   }
 }
 
+// Buffered top-K selection.  A candidate can only enter a lane's list if it
+// beats the list's last entry, so the scan filters against that threshold and
+// APPENDS passing (distance, index) pairs to a per-lane LDS queue; the queue
+// is drained into the sorted register list (topk_insert) only when some lane
+// of the wave nears CAP entries, and after the last candidate.  Between
+// drains the list does not change, so the filter is exactly the insertion
+// test; the queue keeps scan order, so strict-'<' insertion still yields the
+// (distance, index) order of a sequential scan.  What this buys: the
+// 16-deep compare-swap network runs once per *passing* candidate per drain
+// round instead of once per candidate whenever ANY lane of the wave inserts
+// (with ~5 % of candidates passing per lane, ~95 % of a wave's candidate
+// steps used to pay the whole network).
+template <int KK, int CAP, int NT>
+struct TopK {
+  float bd[KK];
+  int bi[KK];
+  float thr;
+  int cnt;
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+      bd[k] = INFINITY;
+      bi[k] = 0;
+    }
+    thr = INFINITY;
+    cnt = 0;
+  }
+  // queue[j * NT + tid]: lane tid's j-th pending candidate
+  __device__ __forceinline__ void offer(int2 *queue, int tid, float d, int k) {
+    if (d < thr) {
+      queue[cnt * NT + tid] = make_int2(__float_as_int(d), k);
+      ++cnt;
+    }
+  }
+  __device__ __forceinline__ void drain(const int2 *queue, int tid) {
+    for (int j = 0; __any(j < cnt); ++j) {
+      if (j < cnt) {
+        const int2 v = queue[j * NT + tid];
+        topk_insert<KK>(bd, bi, __int_as_float(v.x), v.y);
+      }
+    }
+    thr = bd[KK - 1];
+    cnt = 0;
+  }
+  // drain when a further `room` offers could overflow some lane's queue
+  __device__ __forceinline__ void maybe_drain(const int2 *queue, int tid, int room) {
+    if (__any(cnt > CAP - room)) drain(queue, tid);
+  }
+};
+
 // C == 3: candidates staged as float4 (x, y, z, |p|^2)
 template <int KK, int G>
 __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
                                                       int N, int K, int pad, int *__restrict__ idx,
                                                       float *__restrict__ dist) {
-  constexpr int TN = 1024, SL = TN / G;
+  constexpr int TN = 1024, SL = TN / G, U = 8, CAP = 16, NT = 64 * G;
   __shared__ float4 tile[TN];
-  __shared__ MergeBuf<KK, G> mb;
-  const int b = blockIdx.y;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __shared__ union {
+    MergeBuf<KK, G> mb;
+    int2 queue[CAP * NT];
+  } sh;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63;
   const int s = blockIdx.x * 64 + lane;
   const float *qb = q + (size_t)b * S * 3;
   const float *pb = p + (size_t)b * N * 3;
@@ -152,31 +205,33 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
   const float qx = qb[3 * sc], qy = qb[3 * sc + 1], qz = qb[3 * sc + 2];
   const float qn = (qx * qx + qy * qy) + qz * qz;
   const float mx = -2.f * qx, my = -2.f * qy, mz = -2.f * qz;  // (-2q).p == -2(q.p) bit-exactly
-  float bd[KK];
-  int bi[KK];
-#pragma unroll
-  for (int k = 0; k < KK; ++k) {
-    bd[k] = INFINITY;
-    bi[k] = 0;
-  }
+  TopK<KK, CAP, NT> tk;
+  tk.init();
   for (int t0 = 0; t0 < N; t0 += TN) {
     const int cnt = min(TN, N - t0);
-    for (int e = threadIdx.x; e < cnt; e += 64 * G) {
+    for (int e = tid; e < cnt; e += NT) {
       const float *src = pb + (size_t)(t0 + e) * 3;
       const float x = src[0], y = src[1], z = src[2];
       tile[e] = make_float4(x, y, z, (x * x + y * y) + z * z);
     }
     __syncthreads();
-    const int e1 = min(cnt, (w + 1) * SL);
-    for (int e = w * SL; e < e1; ++e) {
-      const float4 c = tile[e];
-      const float dot = __builtin_fmaf(mz, c.z, __builtin_fmaf(my, c.y, mx * c.x));
-      const float d = (dot + qn) + c.w;
-      topk_insert<KK>(bd, bi, d, t0 + e);
+    const int e1 = min(cnt, (w + 1) * SL);  // wave-uniform
+    for (int e0 = w * SL; e0 < e1; e0 += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u;
+        if (e < e1) {
+          const float4 c = tile[e];
+          const float dot = __builtin_fmaf(mz, c.z, __builtin_fmaf(my, c.y, mx * c.x));
+          tk.offer(sh.queue, tid, (dot + qn) + c.w, t0 + e);
+        }
+      }
+      tk.maybe_drain(sh.queue, tid, U);
     }
     __syncthreads();
   }
-  merge_and_store<KK, G>(mb, bd, bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
+  tk.drain(sh.queue, tid);
+  merge_and_store<KK, G>(sh.mb, tk.bd, tk.bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
                          dist ? dist + ((size_t)b * S + sc) * K : nullptr);
 }
 
@@ -274,7 +329,11 @@ __global__ __launch_bounds__(256) void knnC2_kernel(const float *__restrict__ q,
   __shared__ __attribute__((aligned(16))) float sp[CT * LS];
   __shared__ float sd[QT][CT + 1];
   __shared__ float sqn[QT], spn[CT];
-  __shared__ MergeBuf<KK, 4> mb;
+  constexpr int CAP = 16, NT = 256;
+  __shared__ union {
+    MergeBuf<KK, 4> mb;
+    int2 queue[CAP * NT];
+  } sh;
   const int b = blockIdx.y, t = threadIdx.x, tq = t >> 4, tc = t & 15;
   const int w = t >> 6, lane = t & 63;
   const int q0 = blockIdx.x * QT;
@@ -283,13 +342,8 @@ __global__ __launch_bounds__(256) void knnC2_kernel(const float *__restrict__ q,
   const int s = q0 + lane;
   const int sc = s < S ? s : S - 1;
   if (t < QT) sqn[t] = torch_sumsq(qb + (size_t)sc * C, C);
-  float bd[KK];
-  int bi[KK];
-#pragma unroll
-  for (int k = 0; k < KK; ++k) {
-    bd[k] = INFINITY;
-    bi[k] = 0;
-  }
+  TopK<KK, CAP, NT> tk;
+  tk.init();
   for (int t0 = 0; t0 < N; t0 += CT) {
     if (t < CT) spn[t] = t0 + t < N ? torch_sumsq(pb + (size_t)(t0 + t) * C, C) : 0.f;
     float acc[4][4];
@@ -339,14 +393,16 @@ __global__ __launch_bounds__(256) void knnC2_kernel(const float *__restrict__ q,
         sd[tq + 16 * i][tc + 16 * j] = ((-2.f * acc[i][j]) + sqn[tq + 16 * i]) + spn[tc + 16 * j];
     __syncthreads();
     const int e1 = min(CT, N - t0);
-#pragma unroll 4
+#pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int e = w * 16 + k;
-      if (e < e1) topk_insert<KK>(bd, bi, sd[lane][e], t0 + e);
+      if (e < e1) tk.offer(sh.queue, t, sd[lane][e], t0 + e);
+      if (k == 7 || k == 15) tk.maybe_drain(sh.queue, t, 8);
     }
     __syncthreads();
   }
-  merge_and_store<KK, 4>(mb, bd, bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
+  tk.drain(sh.queue, t);
+  merge_and_store<KK, 4>(sh.mb, tk.bd, tk.bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
                          dist ? dist + ((size_t)b * S + sc) * K : nullptr);
 }
 

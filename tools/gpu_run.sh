@@ -3,6 +3,7 @@
 #   bash tools/gpu_run.sh <out-dir> <stage> [<stage> ...]
 # Stages (each under its own time limit; the chain stops at the first failure):
 #   tests        pytest -m gpu (thread timeouts, names a hung test)
+#   tests_k      pytest -m gpu -k "$PYTEST_K"
 #   smoke        __graft_entry__.smoke()
 #   probe        tools/valu_probe (VALU issue cost per instruction kind)
 #   bench        bench.py default line (PCN, N=1)
@@ -22,6 +23,8 @@ run_stage() {
   case "$1" in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
              > "$OUT/pytest_gpu.log" 2>&1 ;;
+    tests_k) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+             -k "${PYTEST_K:?set PYTEST_K}" > "$OUT/pytest_gpu_k.log" 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$OUT/smoke.log" 2>&1 ;;
     probe) timeout -k 10 60 ./tools/valu_probe > "$OUT/valu_probe.txt" 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
