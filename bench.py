@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="samples per GPU (32 PCN, 16 ShapeNet-55)")
     ap.add_argument("--fp32", action="store_true", help="no bf16 autocast (configs[1] numerics)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32-leg", action="store_true",
+                    help="skip the configs[1] figure (fp32 forward + loss, B=16) reported beside the bf16 step")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="issue every launch from Python (no HIP graph)")
@@ -64,6 +66,15 @@ def parse():
                     help="PyTorch TunableOp for the dense GEMMs: 'use' the committed per-shape hipBLASLt "
                          "selections in tuning/ (if present), 'tune' them during warm-up (rank 0 "
                          "writes the file), or 'off' (library heuristics)")
+    ap.add_argument("--overlap", choices=("auto", "off"), default="auto",
+                    help="N>1 (or --dist-selftest): 'auto' all-reduces the gradient bucket by bucket from "
+                         "backward hooks, inside the captured graph (train.BucketedAllReduce), falling back "
+                         "to one all-reduce between the graph replays if capture refuses it; 'off' always "
+                         "uses the single all-reduce")
+    ap.add_argument("--bucket-mb", type=float, default=25.0, help="gradient bucket size for --overlap auto")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="initialise an RCCL process group even at N=1 (exercises the collective path "
+                         "and its graph capture on a one-GPU box)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1_final_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
@@ -133,6 +144,7 @@ def kernel_work(name, a):
       FPS             16 B per point-iteration, B*N*M of them (HBM model)
       Chamfer fwd     8 FLOP per pair, 2*B*N*M pairs (both directions)
       kNN             (2C+2) FLOP per (query, candidate) pair (distance part)
+      glue kernels    bytes that must cross HBM once (each branch states its count)
     """
     if name in ATTN_ARGS:
         i = ATTN_ARGS[name]  # position of B; then H, Lq, Lk, D, scale, dtype
@@ -159,14 +171,57 @@ def kernel_work(name, a):
     if name == "knn":
         B, S, N, C = a[2], a[3], a[4], a[5]
         return (2.0 * C + 2) * B * S * N, "TFLOP/s", VALU_F32_PEAK, "valu"
+    # ---- HBM-bound glue kernels: bytes that must cross HBM once (reads + writes)
+    es = lambda code: 2 if code == 1 else 4  # dtype code 0 = fp32, 1 = bf16  # noqa: E731
+    if name == "colsum":        # g, gdt, rows, C, out, outdt: read the (rows, C) gradient once
+        return float(a[2] * a[3] * es(a[1]) + a[3] * es(a[5])), "GB/s", HBM_PEAK, "hbm"
+    if name == "transpose_add":  # a, adt, b, bdt, out, odt, out2, o2dt, B, R, C
+        n = a[8] * a[9] * a[10]
+        per = es(a[1]) + (es(a[3]) if a[2] else 0) + es(a[5]) + (es(a[7]) if a[6] else 0)
+        return float(n * per), "GB/s", HBM_PEAK, "hbm"
+    if name == "pcsa_forward":   # x, xdt, gates, gdt, basis, patches, K, C, out: read x, write out
+        n = a[5] * a[6] * a[7]
+        return float(2 * n * es(a[1]) + a[5] * a[6] * es(a[3])), "GB/s", HBM_PEAK, "hbm"
+    if name == "pcsa_backward":  # x, xdt, g, gdt, gates, gatesdt, basis, patches, K, C, dx, dgates
+        n = a[7] * a[8] * a[9]
+        return float(n * (2 * es(a[1]) + es(a[3])) + 2 * a[7] * a[8] * es(a[5])), "GB/s", HBM_PEAK, "hbm"
+    if name == "gather_points":  # features, idx, B, C, N, M: 4 B per index + read value + write out
+        B, C, M = a[2], a[3], a[5]
+        return float(4 * B * M + 8 * B * C * M), "GB/s", HBM_PEAK, "hbm"
+    if name == "gather_points_grad":  # grad_out, idx, B, C, N, M, out: zero out, read grad + idx, scatter-add
+        B, C, N, M = a[2], a[3], a[4], a[5]
+        return float(4 * B * C * N + 4 * B * M + 8 * B * C * M), "GB/s", HBM_PEAK, "hbm"
+    if name == "group_points":   # features, idx, B, C, N, S, K
+        B, C, S, K = a[2], a[3], a[5], a[6]
+        return float(4 * B * S * K + 8 * B * C * S * K), "GB/s", HBM_PEAK, "hbm"
+    if name == "group_points_grad":
+        B, C, N, S, K = a[2], a[3], a[4], a[5], a[6]
+        return float(4 * B * C * N + 4 * B * S * K + 8 * B * C * S * K), "GB/s", HBM_PEAK, "hbm"
+    if name == "chamfer_3D.backward":  # xyz1, xyz2, B, n, m: per point read xyz, partner xyz, grad, idx; write own
+        B, n, m = a[2], a[3], a[4]       # grad, scatter-add the partner's (12 + 12 + 4 + 4 + 12 + 12 B)
+        return float(56 * B * (n + m)), "GB/s", HBM_PEAK, "hbm"
+    if name == "points2depth":   # points, rot, trans, B, N, V, H, W: read the cloud, accumulate 8 B / pixel
+        B, N, V, H, W = a[3], a[4], a[5], a[6], a[7]  # (written + re-read), write the image
+        return float(12 * B * N + 20 * B * V * H * W), "GB/s", HBM_PEAK, "hbm"
+    if name == "points2grid":    # points, rot, rot2, trans, B, N, V, R, D: read cloud, write the voxel grid
+        B, N, V, R, D = a[4], a[5], a[6], a[7], a[8]
+        return float(12 * B * N + 4 * B * V * D * R * R), "GB/s", HBM_PEAK, "hbm"
+    if name == "grid2image":     # grid, kern, BV, D, R: read the grid, write 3-channel image
+        BV, D, R = a[2], a[3], a[4]
+        return float(4 * BV * D * R * R + 12 * BV * R * R), "GB/s", HBM_PEAK, "hbm"
     return None
 
 
 # libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
-            "attention bwd dkv": "attn_dkv2_kernel", "furthest_point_sampling": "fps_reg_kernel",
-            "chamfer_3D.forward": "chamfer_nn_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
-            "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel"}
+            "attention bwd dkv": "attn_dkv2_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
+            "chamfer_3D.forward": "chamfer_(nn|screen)_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
+            "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel", "colsum": "colsum",
+            "transpose_add": "transpose_add", "pcsa_forward": "pcsa_fwd", "pcsa_backward": "pcsa_bwd",
+            "gather_points": "gather_kernel", "gather_points_grad": "gather_grad_kernel",
+            "group_points": "group_kernel", "group_points_grad": "group_grad_kernel",
+            "chamfer_3D.backward": "chamfer_grad", "points2depth": "depth_", "points2grid": "points2grid",
+            "grid2image": "grid2image|image_normalize"}
 
 
 def pmc_traffic(path, key, name):
@@ -234,10 +289,10 @@ class Workload:
             self.desc = ("PointSea ShapeNet-55 train step: seprate_point_cloud + PCViews_Real render + fwd + "
                          "get_loss_PM + bwd + AdamW")
 
-    def optimizer(self, params, **kw):
+    def optimizer(self, params, lr=1e-4, **kw):
         if self.name == "svdformer":   # train_pcn.py:57-60
-            return torch.optim.Adam(params, lr=1e-4, betas=(0.9, 0.999), weight_decay=0, **kw)
-        return torch.optim.AdamW(params, lr=1e-4, weight_decay=0.0005, **kw)   # train_55.py:86-88
+            return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), weight_decay=0, **kw)
+        return torch.optim.AdamW(params, lr=lr, weight_decay=0.0005, **kw)   # train_55.py:86-88
 
     def images(self, partial, cpu=False):
         if cpu:
@@ -298,6 +353,46 @@ def cpu_baseline(wl, steps):
             "sample": f"{steps} train steps of 1 {wl.name} sample (2048->{wl.n_out}) after 1 warm-up, fp32: "
                       f"torch CPU ({nthreads} threads) + oracle/pcops_oracle.c point ops (1 thread) + torch CPU "
                       f"attention"}
+
+
+# ------------------------------------------------------------------ configs[1] leg
+def fp32_forward_loss(wl, model, partial, gt, device, steps, use_graph, batch=16):
+    """BASELINE configs[1]: SVDFormer forward + get_loss on a PCN-shaped batch of
+    16, fp32 throughout (no autocast; the fp32 master weights; exact-f32 MFMA
+    attention core), timed per step with the inputs resident in HBM.  Captured
+    in a HIP graph like the train step when the step is."""
+    x, g = partial[:batch].contiguous(), gt[:batch].contiguous()
+    was_training = model.training
+    model.eval()   # forward + loss as the evaluation loop runs it (no BN-statistics update)
+
+    def fwd():
+        with torch.no_grad():
+            depth = wl.images(x)
+            return wl.loss(model(x, depth), x, g)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            fwd()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    run = fwd
+    if use_graph:
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            fwd()
+        run = gr.replay
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    model.train(was_training)
+    return {"config": "BASELINE configs[1]: SVDFormer forward + get_loss, PCN shapes, fp32", "batch": batch,
+            "steps": steps, "ms_per_step": round(dt * 1e3, 3), "samples_per_s": round(batch / dt, 2),
+            "execution": "hip_graph" if use_graph else "eager"}
 
 
 # ------------------------------------------------------------------ GEMM selection
@@ -365,8 +460,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.dist_selftest
+    if use_dist:
         torch.cuda.set_device(local)
+        if args.dist_selftest and "MASTER_ADDR" not in os.environ:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
@@ -392,13 +490,21 @@ def main():
     fp = FlatParams(model, device, bf16=amp)
     use_graph = not args.no_graph
     # one parameter group, elementwise update: Adam over the flat master buffer
-    opt = wl.optimizer([fp.master()], fused=True, capturable=use_graph)
+    # the LR is a device tensor so the captured optimizer graph reads the value
+    # the schedule writes each step (warm-up per batch, train_pcn.py:132-134)
+    opt = wl.optimizer([fp.master()], lr=torch.tensor(1e-4, device=device) if use_graph else 1e-4, fused=True,
+                       capturable=use_graph)
+    from svdformer_pointsea_amd.train import TrainSchedule
+    schedule = TrainSchedule(opt, args.model)
     partial, gt = wl.synth(args.batch, 1000 + rank, device)
     # ShapeNet-55 re-crops its partial input from gt inside the step; the crop
     # draws come from the device's default generator (graph-capturable)
     crop_rng = torch.cuda.default_generators[device.index] if args.model == "pointsea" else None
     loss_acc = torch.zeros((), device=device)
     progress(f"{args.model}: {nparams} parameters; eager warm-up (MIOpen algorithm search)")
+
+    from svdformer_pointsea_amd.train import BucketedAllReduce
+    sync = [BucketedAllReduce(fp, world, bucket_mb=args.bucket_mb) if use_dist and args.overlap == "auto" else None]
 
     def fwd_bwd():
         fp.zero_grad()
@@ -413,13 +519,21 @@ def main():
             pcds = fp.forward(inp, depth)
             loss = wl.loss(pcds, inp, gt, br.join(*gts))
         loss.backward()
-        fp.collect()
+        if sync[0] is not None:
+            sync[0].finish()   # the bucketed all-reduces were issued during backward
+        else:
+            fp.collect()
         loss_acc.add_(loss.detach())  # logged without a host sync
+
+    def grad_sync():
+        if use_dist and sync[0] is None:
+            fp.allreduce(world)
 
     def eager_step():
         fwd_bwd()
-        fp.allreduce(world)
+        grad_sync()
         opt.step()
+        schedule.batch_end()
 
     if use_graph:
         # The host cannot issue the ~3k launches of a step faster than the GPU
@@ -436,15 +550,39 @@ def main():
         torch.cuda.synchronize()
         progress("eager warm-up done; capturing the step")
         g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fb):
-            fwd_bwd()
+        # RCCL's watchdog thread polls the warm-up collectives' events; under
+        # "global" capture such a call from another thread invalidates the
+        # capture, so collectives are captured in thread-local mode, after
+        # the warm-up work has drained
+        cap_mode = "global"
+        if sync[0] is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+            time.sleep(1.0)
+            cap_mode = "thread_local"
+        try:
+            with torch.cuda.graph(g_fb, capture_error_mode=cap_mode):
+                fwd_bwd()
+        except RuntimeError as exc:
+            if sync[0] is None:
+                raise
+            # the collectives could not be captured: one all-reduce between replays
+            progress(f"capture with in-graph all-reduce failed ({exc}); single all-reduce after the replay")
+            for h in sync[0]._hooks:
+                h.remove()
+            sync[0] = None
+            torch.cuda.synchronize()
+            g_fb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_fb):
+                fwd_bwd()
         with torch.cuda.graph(g_opt):
             opt.step()
 
         def step():
             g_fb.replay()
-            fp.allreduce(world)
+            grad_sync()
             g_opt.replay()
+            schedule.batch_end()
         span_steps = args.timing_steps
     else:
         step = eager_step
@@ -454,7 +592,7 @@ def main():
             _lib.KernelTimer.enable()
         span_steps = args.steps
 
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     progress(f"timing {args.steps} steps")
@@ -464,7 +602,7 @@ def main():
         h0 = time.perf_counter()
         step()
         host += time.perf_counter() - h0
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -478,13 +616,18 @@ def main():
         torch.cuda.synchronize()
     spans = _lib.KernelTimer.spans or {}
     _lib.KernelTimer.disable()
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     if not math.isfinite(loss_acc.item()):
         raise RuntimeError("non-finite loss in the timed steps")
 
+    fp32_leg = None
+    if args.model == "svdformer" and not args.fp32 and not args.no_fp32_leg:
+        progress("configs[1] leg: fp32 forward + get_loss, B=16")
+        fp32_leg = fp32_forward_loss(wl, model, partial, gt, device, steps=max(3, args.steps // 2),
+                                     use_graph=use_graph)
     rows = kernel_table(spans)
     out = None
     if rank == 0:
@@ -499,6 +642,10 @@ def main():
             "ms_per_step": elapsed * 1e3 / args.steps,
             "host_issue_ms_per_step": host * 1e3 / args.steps,
             "execution": "hip_graph" if use_graph else "eager",
+            "grad_sync": ("none (single GPU)" if not use_dist else
+                          f"bucketed all-reduce from backward hooks ({len(sync[0].buckets)} buckets of "
+                          f"<= {args.bucket_mb:g} MB){' inside the captured graph' if use_graph else ''}"
+                          if sync[0] is not None else "one all-reduce of the flat bucket after backward"),
             "gemm_selection": (f"TunableOp ({args.tunableop}): {os.path.relpath(tuned, ROOT)}" if tuned
                                else "hipBLASLt heuristics"),
             "kernel_timing": ("HIP events per libpcops launch, %d eager steps after the timed graph replays"
@@ -524,22 +671,38 @@ def main():
                                "traffic_source": os.path.relpath(args.pmc_json, ROOT) if args.pmc_json else None,
                                "avg_launch_ms": round(d["ms"] / d["launches"], 4),
                                "work_per_launch": d["work"] / d["launches"]}
+            # FPS is M-1 serially dependent rounds: its honest figure is time per round
+            fps = {}
+            for e0, e1, a in spans.get("furthest_point_sampling", []):
+                f = fps.setdefault(f"B{a[1]} {a[2]}->{a[3]}", [0, 0.0, a[3]])
+                f[0] += 1
+                f[1] += e0.elapsed_time(e1)
+            out["fps_us_per_round"] = {k: round(v[1] * 1e3 / v[0] / max(1, v[2] - 1), 3) for k, v in fps.items()}
             group = [r for r in timed.values() if r["name"] in ("furthest_point_sampling", "knn",
                                                                  "chamfer_3D.forward")]
             if group:
                 out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) /
                                                          sum(r["ms"] for r in group), 4)
             step_ms = elapsed * 1e3 / args.steps
+            def pmc_row(k, r):
+                t = pmc_traffic(args.pmc_json, k, r["name"])
+                if t is None or not r.get("work") or r.get("unit") != "GB/s":
+                    return {}
+                return {"pmc_traffic_ratio": round(t / (r["work"] / r["launches"]), 3)}
+
             out["kernels"] = {k: {"launches_per_step": r["launches"] / span_steps,
                                   "ms_per_step": round(r["ms"] / span_steps, 4),
                                   "share": round(r["ms"] / span_steps / step_ms, 4),
-                                  **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {})}
+                                  **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {}),
+                                  **pmc_row(k, r)}
                               for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
+        if fp32_leg is not None:
+            out["fp32_forward_loss"] = fp32_leg
         if world == 1 and not args.no_cpu_baseline:
             progress(f"timed {out['ms_per_step']:.2f} ms/step; CPU baseline")
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_steps)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

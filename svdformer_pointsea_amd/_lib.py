@@ -215,9 +215,13 @@ class fork:
 class Workspace:
     """Per-device scratch arena reused across calls (grown, never shrunk).
 
-    Keyed by (device, stream) so concurrent streams never share bytes."""
+    Keyed by (device, stream) so concurrent streams never share bytes.  A
+    buffer that is outgrown is retired, not freed: a HIP graph captured
+    earlier may still replay kernels that write to it, so its memory must
+    never return to the caching allocator."""
 
     _bufs = {}
+    _retired = []
 
     @classmethod
     def get(cls, device, nbytes):
@@ -226,6 +230,8 @@ class Workspace:
         key = (device, torch.cuda.current_stream(device).cuda_stream)
         buf = cls._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
+            if buf is not None:
+                cls._retired.append(buf)
             buf = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
             cls._bufs[key] = buf
         return buf

@@ -13,6 +13,8 @@
 //
 // Backward: own-point terms with plain stores, partner terms with float
 // atomics (the reference uses atomics for both, chamfer3D.cu:155-174).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -106,6 +108,184 @@ __global__ __launch_bounds__(kThreads) void chamfer_nn_kernel(const float *__res
   }
 }
 
+
+// ---------------------------------------------------------------- screened
+// Screened nearest-neighbour search (the default for the large launches).
+// The reference's distance |a - t|^2 costs 3 sub + mul + 2 fma + min = 7 VALU
+// per pair; packed f32 does not help (v_pk_* issue at half rate on gfx950,
+// measured: same wall time).  The screen instead ranks targets by
+//     e(t) = |t|^2 - 2 a.t      (= |a - t|^2 - |a|^2 in exact arithmetic)
+// with |t|^2 precomputed per tile: 3 fma + 1/2 v_min3 = 3.5 VALU per pair.
+// e is a different fp32 expression, so it only SELECTS: per 32-target
+// sub-tile the minimum of e is compared with the query's running minimum plus
+// a rigorous rounding margin, and the sub-tiles that may hold the exact
+// argmin are remembered (4 slots per query).  After the sweep the winner is
+// re-derived with the reference expression (sqd3) over those sub-tiles only,
+// lowest index on equal distances -- the reference's bits and tie rule.
+//
+// Margin: with u = 2^-24, |t| <= Tm (running max over the tiles seen), the fp32
+// e of any target is within eps = 16u (Tm^2 + |a| Tm) of its exact value, and
+// the direct fp32 distance within 8u D of the exact D.  If k* is the direct
+// argmin, e(k*) <= min e + 2 eps + 16u (min e + |a|^2 + eps), the slack every
+// keep / prune test below allows.  A query whose slots overflow (near-ties
+// across > 4 sub-tiles) or is not finite is re-derived by a full direct scan.
+constexpr int kSlots = 4;
+constexpr float kU = 5.9604645e-8f;  // 2^-24
+
+__device__ __forceinline__ float screen_slack(float mine, float an, float eps) {
+  return 2.f * eps + 16.f * kU * fmaxf(0.f, mine + an + eps);
+}
+
+template <int Q>
+__global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *__restrict__ xyz1,
+                                                                  const float *__restrict__ xyz2, int N, int M,
+                                                                  float *__restrict__ dist1, float *__restrict__ dist2,
+                                                                  int *__restrict__ idx1, int *__restrict__ idx2,
+                                                                  int blocks_dir0) {
+  const int b = blockIdx.y;
+  const bool dir = (int)blockIdx.x >= blocks_dir0;
+  const int bx = dir ? blockIdx.x - blocks_dir0 : blockIdx.x;
+  const int NA = dir ? M : N, NT = dir ? N : M;
+  const float *A = (dir ? xyz2 : xyz1) + (size_t)b * NA * 3;
+  const float *T = (dir ? xyz1 : xyz2) + (size_t)b * NT * 3;
+  float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
+  int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
+  if (NT <= 0) return;
+
+  const int tid = threadIdx.x;
+  float ax[Q], ay[Q], az[Q], an[Q], anorm[Q], mine[Q], slack[Q];
+  float mx[Q], my[Q], mz[Q];
+  float cm[Q][kSlots];
+  int cs[Q][kSlots];
+  bool over[Q];
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int qi = bx * kThreads * Q + i * kThreads + tid;
+    const int qc = qi < NA ? qi : NA - 1;
+    ax[i] = A[3 * qc];
+    ay[i] = A[3 * qc + 1];
+    az[i] = A[3 * qc + 2];
+    mx[i] = -2.f * ax[i];
+    my[i] = -2.f * ay[i];
+    mz[i] = -2.f * az[i];
+    an[i] = (ax[i] * ax[i] + ay[i] * ay[i]) + az[i] * az[i];
+    anorm[i] = sqrtf(an[i]);
+    mine[i] = INFINITY;
+    slack[i] = INFINITY;
+    over[i] = !(an[i] < INFINITY);  // NaN / inf query: direct scan
+#pragma unroll
+    for (int c = 0; c < kSlots; ++c) {
+      cm[i][c] = INFINITY;
+      cs[i][c] = -1;
+    }
+  }
+
+  __shared__ float4 tile[kTile];
+  __shared__ float tmax_s[kThreads / 64];
+  float eps_t2 = 0.f;  // running max |t|^2 over the tiles seen (wave-uniform)
+  for (int t0 = 0; t0 < NT; t0 += kTile) {
+    const int cnt = min(kTile, NT - t0);
+    float lmax = 0.f;
+    for (int e = tid; e < kTile; e += kThreads) {
+      float4 v = make_float4(0.f, 0.f, 0.f, INFINITY);  // padding: e = +inf, never a minimum
+      if (e < cnt) {
+        const float *src = T + (size_t)(t0 + e) * 3;
+        v = make_float4(src[0], src[1], src[2], 0.f);
+        v.w = (v.x * v.x + v.y * v.y) + v.z * v.z;
+        lmax = fmaxf(lmax, v.w);
+      }
+      tile[e] = v;
+    }
+    lmax = wave_max_f32(lmax);
+    if ((tid & 63) == 0) tmax_s[tid >> 6] = lmax;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) eps_t2 = fmaxf(eps_t2, tmax_s[w]);
+    const float tm = sqrtf(eps_t2);
+    float eps[Q];
+#pragma unroll
+    for (int i = 0; i < Q; ++i) {
+      eps[i] = 16.f * kU * (eps_t2 + anorm[i] * tm);
+      slack[i] = screen_slack(mine[i], an[i], eps[i]);  // eps only grows: re-derive
+    }
+    const int nsub = (cnt + kSub - 1) / kSub;
+    for (int sb = 0; sb < nsub; ++sb) {
+      float m[Q];
+#pragma unroll
+      for (int i = 0; i < Q; ++i) m[i] = INFINITY;
+#pragma unroll 4
+      for (int kk = 0; kk < kSub; kk += 2) {
+        const float4 p0 = tile[sb * kSub + kk], p1 = tile[sb * kSub + kk + 1];
+#pragma unroll
+        for (int i = 0; i < Q; ++i) {
+          const float e0 = __builtin_fmaf(mz[i], p0.z, __builtin_fmaf(my[i], p0.y, __builtin_fmaf(mx[i], p0.x, p0.w)));
+          const float e1 = __builtin_fmaf(mz[i], p1.z, __builtin_fmaf(my[i], p1.y, __builtin_fmaf(mx[i], p1.x, p1.w)));
+          m[i] = fminf(fminf(m[i], e0), e1);
+        }
+      }
+      const int sub0 = t0 + sb * kSub;
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        if (m[i] <= mine[i] + slack[i]) {  // rare: this sub-tile may hold the argmin
+          if (m[i] < mine[i]) {
+            mine[i] = m[i];
+            slack[i] = screen_slack(mine[i], an[i], eps[i]);
+#pragma unroll
+            for (int c = 0; c < kSlots; ++c)
+              if (cs[i][c] >= 0 && cm[i][c] > mine[i] + slack[i]) cs[i][c] = -1;  // prune
+          }
+          bool placed = false;
+#pragma unroll
+          for (int c = 0; c < kSlots; ++c) {
+            if (!placed && cs[i][c] < 0) {
+              cs[i][c] = sub0;
+              cm[i][c] = m[i];
+              placed = true;
+            }
+          }
+          over[i] = over[i] || !placed;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // exact re-derivation with the reference expression
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int qi = bx * kThreads * Q + i * kThreads + tid;
+    if (qi >= NA) continue;
+    float best = INFINITY;
+    int bk = 0;
+    if (!over[i]) {
+#pragma unroll
+      for (int c = 0; c < kSlots; ++c) {
+        if (cs[i][c] < 0) continue;
+        const int k0 = cs[i][c], k1 = min(k0 + kSub, NT);
+        for (int k = k0; k < k1; ++k) {
+          const float d = sqd3(T[3 * k] - ax[i], T[3 * k + 1] - ay[i], T[3 * k + 2] - az[i]);
+          if (d < best || (d == best && k < bk)) {
+            best = d;
+            bk = k;
+          }
+        }
+      }
+    }
+    if (over[i] || !(best < INFINITY)) {  // full direct scan (overflow, non-finite data)
+      best = INFINITY;
+      bk = 0;
+      for (int k = 0; k < NT; ++k) {
+        const float d = sqd3(T[3 * k] - ax[i], T[3 * k + 1] - ay[i], T[3 * k + 2] - az[i]);
+        if (d < best) {
+          best = d;
+          bk = k;
+        }
+      }
+    }
+    dist[qi] = best < INFINITY ? best : sqd3(T[3 * bk] - ax[i], T[3 * bk + 1] - ay[i], T[3 * bk + 2] - az[i]);
+    idx[qi] = bk;
+  }
+}
+
 // own terms: grad_self[j] = 2 g_j (x_j - y_idx(j)), both directions
 __global__ void chamfer_grad_own_kernel(const float *__restrict__ xyz1, const float *__restrict__ xyz2, int B, int N,
                                         int M, const float *__restrict__ gd1, const float *__restrict__ gd2,
@@ -179,10 +359,24 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
     Q = 4;
   else if (blocks(2) >= 512)
     Q = 2;
+  if (const char *e = getenv("PCOPS_CHAMFER_Q")) Q = atoi(e);  // A/B experiments: 1, 2, 4, 8
   const int b0 = (N + kThreads * Q - 1) / (kThreads * Q);
   const int b1 = (M + kThreads * Q - 1) / (kThreads * Q);
   const dim3 grid(b0 + b1, B);
-  if (Q == 4)
+  static const bool screen = [] {  // PCOPS_CHAMFER_SCREEN=0: the direct kernel (A/B runs)
+    const char *e = getenv("PCOPS_CHAMFER_SCREEN");
+    return !(e && e[0] == '0');
+  }();
+  if (screen && Q == 4)
+    hipLaunchKernelGGL(chamfer_screen_kernel<4>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1,
+                       idx2, b0);
+  else if (screen && Q == 2)
+    hipLaunchKernelGGL(chamfer_screen_kernel<2>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1,
+                       idx2, b0);
+  else if (Q == 8)
+    hipLaunchKernelGGL(chamfer_nn_kernel<8>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1, idx2,
+                       b0);
+  else if (Q == 4)
     hipLaunchKernelGGL(chamfer_nn_kernel<4>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1, idx2,
                        b0);
   else if (Q == 2)

@@ -16,6 +16,13 @@ __device__ __forceinline__ float sqd3(float a, float b, float c) {
   return __builtin_fmaf(c, c, __builtin_fmaf(a, a, b * b));
 }
 
+// packed form of sqd3 on two independent (a, b, c) triples: v_pk_mul_f32 +
+// 2 x v_pk_fma_f32, per-half bit-identical to sqd3
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 sqd3_pk(f32x2 a, f32x2 b, f32x2 c) {
+  return __builtin_elementwise_fma(c, c, __builtin_elementwise_fma(a, a, b * b));
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // ---- wave-level reductions (DPP / swizzle lowered by the compiler) ----

@@ -185,12 +185,15 @@ struct TopK {
   }
 };
 
-// C == 3: candidates staged as float4 (x, y, z, |p|^2)
-template <int KK, int G>
+// C == 3: candidates staged as float4 (x, y, z, |p|^2), TN per tile.
+// Large grids (>= 3 blocks per CU): G = 4, TN = 512 -> 40 KB of LDS, so four
+// blocks (16 waves) fit a CU and the whole grid is resident at once; small
+// grids: G = 8 waves per 64 queries, TN = 1024.
+template <int KK, int G, int TN>
 __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
                                                       int N, int K, int pad, int *__restrict__ idx,
                                                       float *__restrict__ dist) {
-  constexpr int TN = 1024, SL = TN / G, U = 8, CAP = 16, NT = 64 * G;
+  constexpr int SL = TN / G, U = 8, CAP = 16, NT = 64 * G;
   __shared__ float4 tile[TN];
   __shared__ union {
     MergeBuf<KK, G> mb;
@@ -420,7 +423,16 @@ int launch_knn(const float *q, const float *p, int B, int S, int N, int C, int K
   constexpr int G = KK <= 16 ? 4 : (KK <= 32 ? 2 : 1);
   const dim3 grid((S + 63) / 64, B);
   if (C == 3) {
-    hipLaunchKernelGGL((knn3_kernel<KK, G>), grid, dim3(64 * G), 0, st, q, p, S, N, K, pad, idx, dist);
+    if constexpr (KK <= 16) {
+      if ((long)grid.x * grid.y < 768) {  // < 3 blocks per CU: more waves per query
+        hipLaunchKernelGGL((knn3_kernel<KK, 8, 1024>), grid, dim3(512), 0, st, q, p, S, N, K, pad, idx, dist);
+        PC_CHECK_LAUNCH();
+        return PCOPS_OK;
+      }
+      hipLaunchKernelGGL((knn3_kernel<KK, 4, 512>), grid, dim3(256), 0, st, q, p, S, N, K, pad, idx, dist);
+    } else {
+      hipLaunchKernelGGL((knn3_kernel<KK, G, 1024>), grid, dim3(64 * G), 0, st, q, p, S, N, K, pad, idx, dist);
+    }
     PC_CHECK_LAUNCH();
     return PCOPS_OK;
   }

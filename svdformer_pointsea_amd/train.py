@@ -46,24 +46,44 @@ def _bf16_names(model):
     return names
 
 
+def never_used(model):
+    """Parameters the forward never reads: the BatchNorm of a Conv2d block
+    built with if_bn=False (models/model_utils.py:27-43 constructs it anyway).
+    The reference's per-tensor Adam/AdamW skips them (their .grad stays None);
+    FlatParams keeps them out of the optimizer's segment to match."""
+    names = set()
+    for mname, m in model.named_modules():
+        if getattr(m, "if_bn", True) is False and isinstance(getattr(m, "bn", None), nn.Module):
+            for pname, _ in m.bn.named_parameters():
+                names.add(f"{mname}.bn.{pname}" if mname else f"bn.{pname}")
+    return names
+
+
 class FlatParams:
-    def __init__(self, model, device, bf16=True):
+    def __init__(self, model, device, bf16=True, frozen=None):
         self.model = model
         named = list(model.named_parameters())
         low = _bf16_names(model) if bf16 else set()
-        named.sort(key=lambda kv: kv[0] not in low)          # bf16-eligible first (stable)
-        self.n16 = sum(p.numel() for n, p in named if n in low)
+        frozen = never_used(model) if frozen is None else set(frozen)
+        # layout: bf16-eligible | other trainable (fp32) | never-used (stable within each)
+        named.sort(key=lambda kv: (kv[0] in frozen, kv[0] not in low))
+        self.n16 = sum(p.numel() for n, p in named if n in low and n not in frozen)
+        low = low - frozen
         total = sum(p.numel() for _, p in named)
+        self.n_train = total - sum(p.numel() for n, p in named if n in frozen)
+        self.frozen = frozen
         self.flat = torch.empty(total, dtype=torch.float32, device=device)
         self.grad = torch.zeros(total, dtype=torch.float32, device=device)
         self.flat16 = torch.empty(self.n16, dtype=torch.bfloat16, device=device)
         self.grad16 = torch.zeros(self.n16, dtype=torch.bfloat16, device=device)
         self.shadow = {}
         self._order = []   # bf16-eligible shadows in bucket order
+        self._offset = {}  # parameter name -> offset in the flat buffers
         off = 0
         with torch.no_grad():
             for name, p in named:
                 n = p.numel()
+                self._offset[name] = off
                 view = self.flat[off:off + n].as_strided(p.shape, p.stride())
                 view.copy_(p.data)
                 p.data = view
@@ -83,9 +103,11 @@ class FlatParams:
         the per-tensor updates when every parameter is in one param group with
         the same hyper-parameters (train_pcn.py:57-60, train_55.py:86-88), and
         the fused optimizer then runs one kernel over one tensor instead of
-        chunking ~300 tensors (1.0 -> ~0.3 ms per PCN step)."""
-        p = nn.Parameter(self.flat)   # shares the storage
-        p.grad = self.grad
+        chunking ~300 tensors (1.0 -> ~0.3 ms per PCN step).  Parameters the
+        forward never reads sit at the end of the buffer and are left out, as
+        the per-tensor optimizer skips them (AdamW would otherwise decay them)."""
+        p = nn.Parameter(self.flat[:self.n_train])   # shares the storage; never-used tail excluded
+        p.grad = self.grad[:self.n_train]
         return p
 
     def zero_grad(self):
@@ -139,3 +161,253 @@ class FlatParams:
             import torch.distributed as dist
             dist.all_reduce(self.grad)
             self.grad.mul_(1.0 / world)
+
+
+class BucketedAllReduce:
+    """The data-parallel gradient all-reduce, overlapped with backward.
+
+    The flat gradient bucket is cut into contiguous buckets of ~bucket_mb MB
+    (the bf16-eligible region from its END, since the backward pass produces
+    the last layers' gradients first; the fp32 region as one bucket).  A
+    post-accumulate-grad hook on every trainable parameter counts arrivals;
+    when a bucket is complete its bf16 gradients are concatenated and widened
+    into the fp32 bucket (as FlatParams.collect does for all of them at once)
+    and its all-reduce is issued on a communication stream, while the compute
+    stream carries on with the rest of the backward pass.  Buckets are issued
+    strictly in bucket order (a ready bucket waits for its predecessors), so
+    every rank issues the same collectives in the same order.  finish() issues
+    whatever is left (parameters without a gradient contribute zeros) and
+    makes the compute stream wait for the communication stream.
+
+    Sum-then-scale per element, as FlatParams.allreduce: for two ranks the
+    result is bitwise that of the single all-reduce (tests/test_ddp_gloo.py).
+    Works eagerly and inside HIP-graph capture (the hooks run at capture
+    time, so the captured graph holds the collectives)."""
+
+    def __init__(self, fp, world, bucket_mb=25.0, group=None):
+        import torch.distributed as dist
+
+        self.fp, self.world, self.group, self.dist = fp, world, group, dist
+        self.on_gpu = fp.flat.is_cuda
+        self.comm = torch.cuda.Stream(device=fp.flat.device) if self.on_gpu else None
+        # trainable entries in flat order: (offset, numel, tensor that receives the gradient)
+        entries = []
+        shadows = dict(fp.shadow)
+        for n, p in sorted(fp.model.named_parameters(), key=lambda kv: fp._offset[kv[0]]):
+            o = fp._offset[n]
+            if n in fp.frozen:
+                continue
+            entries.append((o, p.numel(), shadows.get(n, p), n in shadows))
+        per = max(1, int(bucket_mb * 2 ** 20 / 4))
+        buckets = []   # (lo, hi, [entries]): contiguous, all bf16 shadows or all fp32 parameters
+        for region in ([e for e in entries if e[3]], [e for e in entries if not e[3]]):
+            cur, hi = [], None
+            for e in reversed(region):                   # back to front: backward order
+                if cur and hi - e[0] > per:
+                    buckets.append((cur[-1][0], hi, cur))
+                    cur, hi = [], None
+                if hi is None:
+                    hi = e[0] + e[1]
+                cur.append(e)
+            if cur:
+                buckets.append((cur[-1][0], hi, cur))
+        self.buckets = buckets
+        self._bucket_of = {}
+        for bi, (_, _, es) in enumerate(buckets):
+            for e in es:
+                self._bucket_of[id(e[2])] = bi
+        self._hooks = []
+        for _, _, es in buckets:
+            for e in es:
+                self._hooks.append(e[2].register_post_accumulate_grad_hook(self._arrived))
+        self.reset()
+
+    def reset(self):
+        self._left = [len(es) for _, _, es in self.buckets]
+        self._events = [[] for _ in self.buckets]
+        self._next = 0
+
+    def _arrived(self, t):
+        bi = self._bucket_of.get(id(t))
+        if bi is None:
+            return
+        if self.on_gpu:
+            # the gradient was produced on the stream backward runs this node on
+            # (the model's side-stream branches differentiate on their own
+            # streams): the bucket's communication work waits for exactly that
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(t.device))
+            self._events[bi].append(ev)
+        self._left[bi] -= 1
+        while self._next < len(self.buckets) and self._left[self._next] == 0:
+            self._issue(self._next)
+            self._next += 1
+
+    def _issue(self, bi):
+        lo, hi, es = self.buckets[bi]
+        fp = self.fp
+        if self.on_gpu:
+            for ev in self._events[bi]:
+                self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                self._reduce(lo, hi, es)
+        else:
+            self._reduce(lo, hi, es)
+
+    def _reduce(self, lo, hi, es):
+        fp = self.fp
+        with torch.no_grad():
+            if es[0][3]:   # bf16 shadows: their gradients into the flat bf16 then the fp32 bucket
+                parts = []
+                for o, n, w, _ in sorted(es, key=lambda e: e[0]):
+                    g = w.grad
+                    parts.append(torch.zeros(n, dtype=fp.grad16.dtype, device=fp.grad16.device)
+                                 if g is None else fp._physical(g, w))
+                torch.cat(parts, out=fp.grad16[lo:hi])
+                fp.grad[lo:hi].copy_(fp.grad16[lo:hi])
+            seg = fp.grad[lo:hi]
+            self.dist.all_reduce(seg, group=self.group)
+            seg.mul_(1.0 / self.world)
+
+    def finish(self):
+        """Issue the buckets still waiting (parameters that got no gradient) and
+        join the communication stream; call after backward()."""
+        if self.on_gpu and self._next < len(self.buckets):
+            self.comm.wait_stream(torch.cuda.current_stream(self.fp.grad.device))
+        while self._next < len(self.buckets):
+            self._issue(self._next)
+            self._next += 1
+        if self.on_gpu:
+            torch.cuda.current_stream(self.fp.grad.device).wait_stream(self.comm)
+        self.reset()
+
+
+# ------------------------------------------------------------------ LR schedules
+class GradualWarmupScheduler(torch.optim.lr_scheduler.LRScheduler):
+    """utils/schedular.py:5-64: linear warm-up of the learning rate over
+    `total_epoch` scheduler steps (from 0 when multiplier == 1), then hand-off to
+    `after_scheduler` (MultiStepLR for PCN, StepLR for ShapeNet-55), whose base
+    LRs become base_lr * multiplier.  Same get_lr / step arithmetic as the
+    reference; ReduceLROnPlateau hand-off is not used by either train loop and
+    is not restated."""
+
+    def __init__(self, optimizer, multiplier, total_epoch, after_scheduler=None):
+        if multiplier < 1.0:
+            raise ValueError("multiplier should be greater thant or equal to 1.")
+        self.multiplier = multiplier
+        self.total_epoch = total_epoch
+        self.after_scheduler = after_scheduler
+        self.finished = False
+        super().__init__(optimizer)
+
+    def get_lr(self):
+        if self.last_epoch > self.total_epoch:
+            if self.after_scheduler:
+                if not self.finished:
+                    self.after_scheduler.base_lrs = [b * self.multiplier for b in self.base_lrs]
+                    self.finished = True
+                return self.after_scheduler.get_last_lr()
+            return [b * self.multiplier for b in self.base_lrs]
+        if self.multiplier == 1.0:
+            return [b * (float(self.last_epoch) / self.total_epoch) for b in self.base_lrs]
+        return [b * ((self.multiplier - 1.0) * self.last_epoch / self.total_epoch + 1.0) for b in self.base_lrs]
+
+    def step(self, epoch=None):
+        if self.finished and self.after_scheduler:
+            self.after_scheduler.step(None if epoch is None else epoch - self.total_epoch)
+            self._last_lr = self.after_scheduler.get_last_lr()
+        else:
+            super().step(epoch)
+
+
+class TrainSchedule:
+    """The reference loops' LR policy around one optimizer
+    (core/train_pcn.py:62-65,132-140; core/train_55.py:90-94,197-205):
+    warm-up scheduler stepped once per batch for the first WARMUP_STEPS
+    batches, then stepped once per epoch (MultiStepLR milestones / StepLR)."""
+
+    def __init__(self, optimizer, model="svdformer", warmup_steps=300):
+        from torch.optim.lr_scheduler import MultiStepLR, StepLR
+
+        if model == "svdformer":   # config_pcn.py:70-73
+            after = MultiStepLR(optimizer, milestones=[40, 80, 120, 160, 200, 240, 280, 320, 360], gamma=0.7)
+        else:                      # config_55.py:70-72
+            after = StepLR(optimizer, step_size=2, gamma=0.98)
+        self.warmup_steps = warmup_steps
+        self.sched = GradualWarmupScheduler(optimizer, multiplier=1, total_epoch=warmup_steps, after_scheduler=after)
+        self.steps = 0
+
+    def batch_end(self):
+        if self.steps <= self.warmup_steps:
+            self.sched.step()
+            self.steps += 1
+
+    def epoch_end(self):
+        self.sched.step()
+
+    def lr(self):
+        v = self.sched.get_last_lr()[0]
+        return float(v)
+
+
+# ------------------------------------------------------------------ checkpoints
+def checkpoint_state(model, optimizer, fp=None, prefix="module."):
+    """The reference's checkpoint dict (core/train_pcn.py:152-166):
+    {'model': state_dict with DataParallel's 'module.' prefix,
+     'optimizer': the state_dict of a per-tensor Adam/AdamW over
+                  model.parameters()}.
+    With FlatParams the optimizer runs on one flat tensor; its moments are
+    split back into per-parameter entries in model.parameters() order, and
+    parameters the forward never reads get no entry (the per-tensor optimizer
+    never creates state for a parameter whose .grad is None)."""
+    sd = {prefix + k: v.detach().clone() for k, v in model.state_dict().items()}
+    osd = optimizer.state_dict()
+    if fp is None:
+        return {"model": sd, "optimizer": osd}
+    names = [n for n, _ in model.named_parameters()]
+    params = dict(model.named_parameters())
+    (flat_state,) = list(osd["state"].values()) or [{}]
+    state = {}
+    for i, n in enumerate(names):
+        if n in fp.frozen or not flat_state:
+            continue
+        o, p = fp._offset[n], params[n]
+        ent = {}
+        for k, v in flat_state.items():
+            if torch.is_tensor(v) and v.numel() == fp.n_train:
+                ent[k] = v[o:o + p.numel()].view_as(p).clone()
+            else:
+                ent[k] = v.clone() if torch.is_tensor(v) else v
+        state[i] = ent
+    (group,) = osd["param_groups"]
+    group = dict(group)
+    group["params"] = list(range(len(names)))
+    return {"model": sd, "optimizer": {"state": state, "param_groups": [group]}}
+
+
+def load_checkpoint_state(ckpt, model, optimizer, fp=None, prefix="module."):
+    """Inverse of checkpoint_state; also reads checkpoints written by the
+    reference's per-tensor optimizer (the same layout)."""
+    sd = {(k[len(prefix):] if k.startswith(prefix) else k): v for k, v in ckpt["model"].items()}
+    model.load_state_dict(sd, strict=True)
+    osd = ckpt["optimizer"]
+    if fp is None:
+        optimizer.load_state_dict(osd)
+        return
+    names = [n for n, _ in model.named_parameters()]
+    params = dict(model.named_parameters())
+    (group,) = osd["param_groups"]
+    flat_state = {}
+    for i, ent in osd["state"].items():
+        n = names[int(i)]
+        o, p = fp._offset[n], params[n]
+        for k, v in ent.items():
+            if torch.is_tensor(v) and v.shape == p.shape:
+                buf = flat_state.setdefault(k, torch.zeros(fp.n_train, dtype=v.dtype, device=fp.flat.device))
+                buf[o:o + p.numel()].view_as(p).copy_(v)
+            else:
+                flat_state[k] = v.clone() if torch.is_tensor(v) else v   # never alias the source's step
+    (cur,) = optimizer.state_dict()["param_groups"]
+    group = {**group, "params": cur["params"]}
+    optimizer.load_state_dict({"state": {cur["params"][0]: flat_state} if flat_state else {},
+                               "param_groups": [group]})

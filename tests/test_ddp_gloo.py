@@ -3,7 +3,8 @@
 Each rank runs the real SVDFormer PCN step on its own sample (point ops on
 the oracle CPU path) with train.FlatParams (bench.py's parameter storage):
 gradients accumulate into one flat buffer whose all-reduce is the step's
-only collective.  After it, the
+only collective -- issued once after backward, or bucket by bucket from
+backward hooks (train.BucketedAllReduce, bitwise the same).  After it, the
 gradients must be identical on both ranks and equal the mean of the ranks'
 local gradients, and one Adam step must leave identical weights."""
 import os
@@ -43,7 +44,23 @@ def _worker(rank, world, port, out):
         loss.backward()
         fp.collect()
     local = fp.grad.clone()
+    # the overlapped path: the same step with bucketed all-reduces issued from
+    # backward hooks (small buckets -> many collectives) must give the single
+    # all-reduce's gradients bitwise
+    from svdformer_pointsea_amd.train import BucketedAllReduce
+
+    sync = BucketedAllReduce(fp, world, bucket_mb=4.0)
+    with cpu_ops():
+        fp.zero_grad()
+        loss, _ = get_loss(fp.forward(partial, depth), gt)
+        loss.backward()
+        sync.finish()
+    bucketed = fp.grad.clone()
+    for h in sync._hooks:
+        h.remove()
+    fp.grad.copy_(local)
     fp.allreduce(world)
+    n_buckets = len(sync.buckets)
     mean_local = local.clone()
     dist.all_reduce(mean_local)
     mean_local /= world
@@ -55,7 +72,8 @@ def _worker(rank, world, port, out):
     w0 = w.clone()
     dist.broadcast(w0, src=0)
     out[rank] = (float((fp.grad - mean_local).abs().max()), float((fp.grad - other).abs().max()),
-                 float(local.abs().max()), float((w - w0).abs().max()))
+                 float(local.abs().max()), float((w - w0).abs().max()),
+                 bool(torch.equal(bucketed[:fp.n_train], fp.grad[:fp.n_train])), n_buckets)
     dist.destroy_process_group()
 
 
@@ -67,6 +85,7 @@ def test_ddp_gloo_world2():
         mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
         res = dict(out)
     for rank in range(world):
-        diff_mean, diff_ranks, scale, diff_w = res[rank]
+        diff_mean, diff_ranks, scale, diff_w, bucketed_equal, n_buckets = res[rank]
         assert diff_ranks == 0.0 and diff_w == 0.0
+        assert bucketed_equal and n_buckets > 5
         assert diff_mean <= 1e-6 * max(scale, 1.0)

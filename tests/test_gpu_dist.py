@@ -1,0 +1,97 @@
+"""The data-parallel gradient path on the GPU with a real RCCL process group
+(one rank: the one-GPU box's stand-in for the 8-GPU node): the bucketed
+all-reduce issued from backward hooks (train.BucketedAllReduce) -- eagerly
+and captured inside a HIP graph -- must give the gradients of the single
+all-reduce after backward, bitwise, on the bf16-shadow + fp32 parameter
+layout bench.py uses."""
+import copy
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+from torch import nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def group(dev):
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                device_id=dev)
+    yield
+    # the group stays for the session (RCCL teardown mid-session is not needed)
+
+
+class _Net(nn.Module):
+    def __init__(self):
+        super().__init__()
+        from svdformer_pointsea_amd.attention import self_attention
+
+        self.blk = self_attention(32, 64, nhead=2)
+        self.norm = nn.LayerNorm(64)
+        self.head = nn.Linear(64, 3)
+        self.side = nn.Linear(32, 48)
+        self.unused = nn.Linear(5, 5)
+
+    def forward(self, x):
+        from svdformer_pointsea_amd import _lib
+
+        # a branch on a side stream (as the model's local encoder): its weight
+        # gradients are produced on that stream during backward
+        with _lib.fork(x.device, lane=3) as br:
+            z = self.side(x.mean(2))
+        y = self.blk(x).transpose(1, 2)
+        return self.head(self.norm(y.float())).float().square().mean() + br.join(z).float().square().mean()
+
+
+def _step(fp, x, sync):
+    fp.zero_grad()
+    fp.refresh()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = fp.forward(x)
+    loss.backward()
+    if sync is None:
+        fp.collect()
+        fp.allreduce(1)
+    else:
+        sync.finish()
+    return loss.detach()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_bucketed_allreduce_rccl(dev, group, graph):
+    from svdformer_pointsea_amd.train import BucketedAllReduce, FlatParams
+
+    torch.manual_seed(0)
+    a = _Net().to(dev)
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 32, 50, device=dev)
+    fa, fb = FlatParams(a, dev), FlatParams(b, dev)
+    _step(fa, x, None)
+    ref = fa.grad.clone()
+    sync = BucketedAllReduce(fb, 1, bucket_mb=0.01)
+    assert len(sync.buckets) > 4
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            _step(fb, x, sync)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(fb.grad, ref)
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            _step(fb, x, sync)
+        fb.grad.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(fb.grad, ref), (fb.grad - ref).abs().max().item()

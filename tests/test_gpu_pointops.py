@@ -179,6 +179,57 @@ def test_chamfer_bitexact_and_backward(dev, B, N, M):
     np.testing.assert_allclose(bt.grad.cpu().numpy(), g2, rtol=1e-5, atol=1e-6)
 
 
+def _screen_clouds(kind, rng):
+    if kind == "uniform":
+        return [(rng.random((2, n, 3)) - 0.5).astype(np.float32) for n in (3000, 5000)]
+    if kind == "tiled":  # every point repeated across many sub-tiles: exact ties, slot overflow
+        return [_tiled(rng, 2, 300, 3000), _tiled(rng, 2, 200, 4100)]
+    if kind == "outliers":  # a few far points inflate the rounding margin
+        a, b = [(rng.random((2, n, 3)) - 0.5).astype(np.float32) for n in (2500, 4000)]
+        b[:, ::997] *= 1000.0
+        a[:, ::501] *= 300.0
+        return [a, b]
+    if kind == "offset":  # tiny cloud far from the origin: margin >> neighbour gaps
+        a, b = [(100.0 + 1e-3 * rng.standard_normal((2, n, 3))).astype(np.float32) for n in (2048, 3000)]
+        return [a, b]
+    if kind == "nonfinite":
+        a, b = [(rng.random((1, n, 3)) - 0.5).astype(np.float32) for n in (2100, 2300)]
+        a[0, 5] = np.nan
+        b[0, 7] = np.nan
+        b[0, 9] = np.inf
+        return [a, b]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("q", ["2", "4"])
+@pytest.mark.parametrize("kind", ["uniform", "tiled", "outliers", "offset", "nonfinite"])
+def test_chamfer_screen_bitexact(dev, monkeypatch, kind, q):
+    """The screened kernel (e = |t|^2 - 2a.t ranks sub-tiles, the reference
+    expression re-derives the winner) forced onto small clouds through
+    PCOPS_CHAMFER_Q: bit-exact distances and indices against the oracle on
+    exact ties, far outliers, a cloud far from the origin and non-finite points."""
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    monkeypatch.setenv("PCOPS_CHAMFER_Q", q)
+    a, b = _screen_clouds(kind, np.random.default_rng(len(kind) * 7 + int(q)))
+    got = [t.cpu().numpy() for t in chamfer_3DDist()(T(a, dev), T(b, dev))]
+    ref = O.chamfer_forward(a, b)
+    for x, y in zip(got, ref):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_chamfer_full_size_one_cloud_bitexact(dev):
+    """16384 x 16384 (the loss Chamfer, screened kernel) on one cloud, both directions, vs the oracle."""
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    a = (torch.randn(1, 16384, 3, generator=g) * 0.45).numpy()
+    b = (torch.randn(1, 16384, 3, generator=g) * 0.45).numpy()
+    got = [t.cpu().numpy() for t in chamfer_3DDist()(T(a, dev), T(b, dev))]
+    for x, y in zip(got, O.chamfer_forward(a, b)):
+        np.testing.assert_array_equal(x, y)
+
+
 def test_chamfer_full_size_properties(dev):
     """B=32, 16384 x 16384 (the loss Chamfer): symmetry and spot checks."""
     from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist

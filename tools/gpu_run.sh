@@ -12,6 +12,8 @@
 #   trace        rocprofv3 --kernel-trace --stats of bench.py
 #   pmc_traffic  two PMC passes (FETCH_SIZE / WRITE_SIZE) -> tools/pmc_traffic.py
 #   pmc_attn     SQ counter pass over the attention kernels (tools/attn_bench.py)
+#   dist1        bench.py under torch.distributed.run with ONE rank and an RCCL group
+#                (--dist-selftest): the bucketed all-reduce captured in the graph
 #   avail        rocprofv3 --list-avail
 #   knn          tools/knn_bench.py ; chamfer: tools/microbench.py chamfer
 set -o pipefail
@@ -47,6 +49,9 @@ run_stage() {
         SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
         --kernel-include-regex 'attn_' --output-format csv -d "$OUT/pmc_attn" -o run -- \
         python tools/attn_bench.py 0 1 > "$OUT/pmc_attn.log" 2>&1 ;;
+    dist1) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+             --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg \
+             > "$OUT/bench_dist1.json" 2> "$OUT/bench_dist1.err" ;;
     avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
     knn) timeout -k 10 120 python tools/knn_bench.py > "$OUT/knn_bench.txt" 2>&1 ;;
     chamfer) timeout -k 10 120 python tools/microbench.py > "$OUT/chamfer_bench.txt" 2>&1 ;;
