@@ -7,6 +7,7 @@ device, so the ops compose with torch kernels, streams and hipGraph capture.
 """
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -169,6 +170,42 @@ def require_int(t, name):
 
 
 _SIDE = {}
+_TLS = threading.local()
+
+
+def on_side_stream():
+    """True inside a `fork` block on this thread (the block's ops run on a side stream)."""
+    return getattr(_TLS, "side", 0) > 0
+
+
+class no_stream_k:
+    """GEMMs issued inside run on rocBLAS instead of hipBLASLt, with TunableOp
+    off.  hipBLASLt's gfx950 bf16 solutions are stream-K (streamK=3 in 208 of
+    the 211 solutions of its Tensile library; 85 of the 88 GEMM kernels a PCN
+    step launches carry _SK3_): workgroups that own a split tile spin-wait for
+    the partial sums of other workgroups of the same launch, which assumes the
+    whole grid becomes resident.  Two such launches on two streams can each
+    hold the CUs the other's producers need -- the recorded graph-replay hang.
+    rocBLAS's gfx950 bf16 Tensile solutions are all streamK=0 (data-parallel,
+    no cross-workgroup waits), so side-stream GEMMs go there and at most one
+    spinning launch is ever in flight.  The switches are process-global; they
+    are flipped around the issue of the side-stream GEMMs only (on the one
+    thread issuing them), including at graph-capture time."""
+
+    def __enter__(self):
+        import torch.cuda.tunable as tunable
+
+        self.prev = (torch.backends.cuda.preferred_blas_library(), tunable.is_enabled())
+        torch.backends.cuda.preferred_blas_library("cublas")
+        tunable.enable(False)
+        return self
+
+    def __exit__(self, *exc):
+        import torch.cuda.tunable as tunable
+
+        torch.backends.cuda.preferred_blas_library(self.prev[0])
+        tunable.enable(self.prev[1])
+        return False
 
 
 def side_stream(device, lane=0):
@@ -185,8 +222,12 @@ class fork:
     current stream's pending work; `join(*tensors)` makes the current stream
     wait for it and marks the tensors as used there.  No-op on CPU tensors."""
 
+    # PCOPS_SIDE_STREAMS=0 runs every block on the current stream (A/B runs, and
+    # the only safe way to put hipBLASLt GEMMs inside a forked block)
+    enabled = os.environ.get("PCOPS_SIDE_STREAMS", "1") != "0"
+
     def __init__(self, device, lane=0):
-        self.on = torch.device(device).type == "cuda"
+        self.on = fork.enabled and torch.device(device).type == "cuda"
         if self.on:
             self.main = torch.cuda.current_stream(device)
             self.side = side_stream(device, lane)
@@ -196,10 +237,12 @@ class fork:
             self.side.wait_stream(self.main)
             self._ctx = torch.cuda.stream(self.side)
             self._ctx.__enter__()
+            _TLS.side = getattr(_TLS, "side", 0) + 1
         return self
 
     def __exit__(self, *exc):
         if self.on:
+            _TLS.side -= 1
             self._ctx.__exit__(*exc)
         return False
 

@@ -76,7 +76,11 @@ class _Linear(Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
-        return F.linear(x, w, b)
+        # on a side stream: GEMMs without stream-K (forward here, backward on
+        # the same stream later -- autograd replays the forward's streams)
+        ctx.side = _lib.on_side_stream()
+        with _lib.no_stream_k() if ctx.side else _nullctx():
+            return F.linear(x, w, b)
 
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
@@ -85,13 +89,22 @@ class _Linear(Function):
         C = g.shape[-1]
         g2 = g.reshape(-1, C)
         gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = (g2 @ w).view(x.shape)
-        if ctx.needs_input_grad[1]:
-            gw = _wgrad(g2.contiguous(), x.reshape(-1, x.shape[-1]).contiguous(), w.dtype)
+        with _lib.no_stream_k() if ctx.side else _nullctx():
+            if ctx.needs_input_grad[0]:
+                gx = (g2 @ w).view(x.shape)
+            if ctx.needs_input_grad[1]:
+                gw = _wgrad(g2.contiguous(), x.reshape(-1, x.shape[-1]).contiguous(), w.dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = colsum(g2.contiguous())
         return gx, gw, gb
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def colsum(g):
@@ -111,7 +124,14 @@ def colsum(g):
 
 def linear(x, w, b=None):
     """F.linear for the blocks' Linear / 1x1-conv layers: the _Linear path when
-    the weight gradient is a long-K GEMM (>= 8192 tokens), else F.linear."""
+    the weight gradient is a long-K GEMM (>= 8192 tokens), else F.linear.
+    Inside a _lib.fork block (a side stream) every GEMM, forward and backward,
+    goes through _lib.no_stream_k."""
+    if _lib.on_side_stream() and x.is_cuda:
+        if torch.is_grad_enabled() and (w.requires_grad or x.requires_grad):
+            return _Linear.apply(x, w, b)      # both directions without stream-K
+        with _lib.no_stream_k():
+            return F.linear(x, w, b)
     if not (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and x.numel() // x.shape[-1] >= 8192):
         return F.linear(x, w, b)
     return _Linear.apply(x, w, b)

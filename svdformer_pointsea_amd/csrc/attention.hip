@@ -18,6 +18,8 @@
 // the parity build.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -378,6 +380,20 @@ constexpr int kKT = 64;  // keys per tile
 #endif
 constexpr float kDeferLog2 = PCOPS_DEFER_LOG2;  // forward: rescale only when a row max grows by > 2^8
 
+// v_exp_f32 directly: exp2f's library form wraps it in a denormal-range
+// rescale (cmp + 2 cndmask + add + ldexp: 6 VALU per probability, 40 % of the
+// forward loop's VALU).  A probability below 2^-126 of its row maximum is
+// flushed to 0 instead -- invisible in bf16 P (and in any fp32 sum of them).
+__device__ __forceinline__ float exp2_ftz(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// v_max3_f32 as ONE instruction: fmaxf on MFMA results makes the compiler
+// canonicalise each operand first (a v_max x, x per score, IEEE mode)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ float swap_halves_max(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -549,7 +565,10 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
   fwd2_store<D, NW>(sk, sv, kr, vr);
   lds_barrier();
   const int ntiles = (Lk + kKT - 1) / kKT;
-  for (int t = 0; t < ntiles; ++t) {
+  // one tile; EDGE: the last, partial tile (key masking), compiled separately
+  // so full tiles carry no per-score mask selects
+  auto tile = [&](int t, auto edge_c) {
+    constexpr bool EDGE = decltype(edge_c)::value;
     const int cur = t & 1;
     const int k0 = t * kKT;
     if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
@@ -558,7 +577,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     f32x16 X0 = f32x16{}, X1 = f32x16{};
     k_product<D>(X0, ck, qf);
     k_product<D>(X1, ck + 32 * C::kKS, qf);
-    if (k0 + kKT > Lk) {
+    if constexpr (EDGE) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (k0 + acc_row(r, h) >= Lk) X0[r] = -INFINITY;
@@ -567,7 +586,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     }
     float tmax = -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(X0[r], X1[r]));
+    for (int r = 0; r < 16; ++r) tmax = max3_raw(tmax, X0[r], X1[r]);
     tmax = swap_halves_max(tmax);
     // deferred max (guide T13): while no row's tile max exceeds its running
     // max by more than kDeferLog2 (P <= 2^8), keep m and skip the O rescale;
@@ -575,12 +594,12 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     const float pm = tmax * sl2;
     const bool keep = __all(pm - m <= kDeferLog2);
     const float mn = keep ? m : fmaxf(m, pm);
-    const float alpha = keep ? 1.f : exp2f(m - mn);
+    const float alpha = keep ? 1.f : exp2_ftz(m - mn);
     float rs = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      X0[r] = exp2f(__builtin_fmaf(X0[r], sl2, -mn));
-      X1[r] = exp2f(__builtin_fmaf(X1[r], sl2, -mn));
+      X0[r] = exp2_ftz(__builtin_fmaf(X0[r], sl2, -mn));
+      X1[r] = exp2_ftz(__builtin_fmaf(X1[r], sl2, -mn));
       rs += X0[r] + X1[r];
     }
     rs = swap_halves_sum(rs);
@@ -594,7 +613,10 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     v_product<D>(Y, cv + 32 * C::kVS, X1);
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
-  }
+  };
+  const int nfull = Lk / kKT;
+  for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
   store_Y<__bf16, D>(Y, O + st.o_off(bh), st.o_srow, q0, Lq, 1.f / lsum);
   if (h == 0 && qi < Lq && lse) lse[(long long)bh * Lq + qi] = (m + log2f(lsum)) * kLn2;
 }
@@ -674,7 +696,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
   fwd2_store<D, NW>(sk, sv, kr, vr);
   lds_barrier();
   const int ntiles = (Lk + kKT - 1) / kKT;
-  for (int t = 0; t < ntiles; ++t) {
+  auto tile = [&](int t, auto edge_c) {
+    constexpr bool EDGE = decltype(edge_c)::value;
     const int cur = t & 1;
     const int k0 = t * kKT;
     if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
@@ -685,12 +708,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
     k_product<D>(S1, ck + 32 * C::kKS, qf);
     k_product<D>(G0, cv, gf);
     k_product<D>(G1, cv + 32 * C::kVS, gf);
-    const bool edge = k0 + kKT > Lk;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float p0 = exp2f(__builtin_fmaf(S0[r], sl2, -lse2));
-      float p1 = exp2f(__builtin_fmaf(S1[r], sl2, -lse2));
-      if (edge) {
+      float p0 = exp2_ftz(__builtin_fmaf(S0[r], sl2, -lse2));
+      float p1 = exp2_ftz(__builtin_fmaf(S1[r], sl2, -lse2));
+      if constexpr (EDGE) {
         if (k0 + acc_row(r, h) >= Lk) p0 = 0.f;
         if (k0 + 32 + acc_row(r, h) >= Lk) p1 = 0.f;
       }
@@ -701,7 +723,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
     v_product<D>(Y, ck + 32 * C::kKS, S1);
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
-  }
+  };
+  const int nfull = Lk / kKT;
+  for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
   store_Y<__bf16, D>(Y, dQ + st.q_off(bh), st.q_srow, q0, Lq, scale);
 }
 
@@ -790,8 +815,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = acc_row(r, h);
-        const float p0 = exp2f(__builtin_fmaf(S0[r], sl2, -cl[row]));  // 0 for rows beyond Lq (lse = +inf)
-        const float p1 = exp2f(__builtin_fmaf(S1[r], sl2, -cl[row + 32]));
+        const float p0 = exp2_ftz(__builtin_fmaf(S0[r], sl2, -cl[row]));  // 0 for rows beyond Lq (lse = +inf)
+        const float p1 = exp2_ftz(__builtin_fmaf(S1[r], sl2, -cl[row + 32]));
         S0[r] = p0;
         S1[r] = p1;
         G0[r] = p0 * (G0[r] - cd[row]);
@@ -812,7 +837,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = acc_row(r, h) + 32 * hf;
-          const float p = exp2f(__builtin_fmaf(S[r], sl2, -cl[row]));
+          const float p = exp2_ftz(__builtin_fmaf(S[r], sl2, -cl[row]));
           S[r] = p;
           if (MODE == 2) G[r] = p * (G[r] - cd[row]);
         }

@@ -224,7 +224,7 @@ class Model(nn.Module):
 
     def forward(self, partial, depth):
         partial_cm = partial.transpose(1, 2).contiguous()
-        # the local encoder (EdgeConv kNN, FPS, MIOpen convs -- no hipBLASLt GEMMs)
+        # the local encoder (EdgeConv kNN, FPS, 1x1-conv GEMMs on rocBLAS: no stream-K)
         # only depends on the partial cloud: it runs on a second HIP stream
         # beside the view/point encoder
         with fork(partial.device) as br:

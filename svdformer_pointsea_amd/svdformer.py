@@ -44,16 +44,12 @@ def max_over_neighbours(x):
 
 import os as _os
 
-# Which 1x1 convs run as GEMMs (A/B switch): sa (default) | all | edge | off.
-# The local encoder's EdgeConvs run on a side stream (Model.forward), and
-# hipBLASLt GEMMs must never run on two streams at once: its stream-K
-# kernels spin-wait on workgroups of the same launch, and two such launches
-# side by side can hold the CUs each other's waiters need (a PointSea graph
-# replay with GEMMs on both streams hung).  So the EdgeConvs stay on MIOpen
-# ("all" measured 68.2 vs 71.3 ms on the PCN step, but is not safe); the
-# side-stream overlap is worth more (local encoder on the main stream with
-# "all": 72.5 ms PCN, 50.9 ms PointSea).
-_CONV1X1 = _os.environ.get("PCOPS_CONV1X1", "sa")
+# Which 1x1 convs run as GEMMs (A/B switch): sa | all (default) | edge | off.
+# The local encoder's EdgeConvs run on a side stream (Model.forward); their
+# GEMMs go through attention.linear, which issues side-stream GEMMs on rocBLAS
+# (no stream-K) -- hipBLASLt's stream-K GEMMs on two streams at once were the
+# recorded PointSea graph-replay hang (_lib.no_stream_k has the mechanism).
+_CONV1X1 = _os.environ.get("PCOPS_CONV1X1", "all")
 
 
 def conv1x1(x, conv, where="sa"):
@@ -506,7 +502,7 @@ class Model(nn.Module):
 
     def forward(self, partial, depth):
         partial_cm = partial.transpose(1, 2).contiguous()
-        # the local encoder (EdgeConv kNN, FPS, MIOpen convs -- no hipBLASLt GEMMs)
+        # the local encoder (EdgeConv kNN, FPS, 1x1-conv GEMMs on rocBLAS: no stream-K)
         # only depends on the partial cloud: it runs on a second HIP stream
         # beside the view/point encoder
         with fork(partial.device) as br:

@@ -31,24 +31,33 @@ run_stage() {
     probe) timeout -k 10 60 ./tools/valu_probe > "$OUT/valu_probe.txt" 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     bench_ps) timeout -k 10 500 python bench.py --model pointsea > "$OUT/bench_pointsea.json" 2> "$OUT/bench_pointsea.err" ;;
+    bench_sa) PCOPS_CONV1X1=sa timeout -k 10 600 python bench.py --no-cpu-baseline --no-fp32-leg > "$OUT/bench_sa.json" \
+             2> "$OUT/bench_sa.err" ;;
+    bench_ps_sa) PCOPS_CONV1X1=sa timeout -k 10 500 python bench.py --model pointsea --no-cpu-baseline \
+             > "$OUT/bench_pointsea_sa.json" 2> "$OUT/bench_pointsea_sa.err" ;;
     bench_fp32) timeout -k 10 500 python bench.py --fp32 --batch 16 --no-cpu-baseline > "$OUT/bench_fp32.json" \
                   2> "$OUT/bench_fp32.err" ;;
     trace) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-             python bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_traced.json" 2> "$OUT/trace.err" ;;
+             python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32-leg > "$OUT/bench_traced.json" \
+             2> "$OUT/trace.err" &&
+           find "$OUT/trace" -name '*kernel_trace.csv' -exec gzip -9 {} + ;;   # keep the merge-back small
     pmc_traffic)
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
         -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
-        > /dev/null 2> "$OUT/pmc_fetch.err" &&
+        --no-fp32-leg > /dev/null 2> "$OUT/pmc_fetch.err" &&
       timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
         -d "$OUT/pmc_write" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
-        > /dev/null 2> "$OUT/pmc_write.err" &&
+        --no-fp32-leg > /dev/null 2> "$OUT/pmc_write.err" &&
       python tools/pmc_traffic.py "$(find "$OUT/pmc_fetch" -name '*counter_collection.csv' -print -quit)" \
-        "$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)" "$OUT/pmc_traffic.json" ;;
+        "$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)" "$OUT/pmc_traffic.json" &&
+      find "$OUT/pmc_fetch" "$OUT/pmc_write" -name '*.csv' -exec gzip -9 {} + ;;
     pmc_attn)
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA \
         SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
         --kernel-include-regex 'attn_' --output-format csv -d "$OUT/pmc_attn" -o run -- \
-        python tools/attn_bench.py 0 1 > "$OUT/pmc_attn.log" 2>&1 ;;
+        python tools/attn_bench.py 0 1 > "$OUT/pmc_attn.log" 2>&1 &&
+      python tools/pmc_attn.py "$(find "$OUT/pmc_attn" -name '*counter_collection.csv' -print -quit)" \
+        > "$OUT/pmc_attn_summary.json" ;;
     dist1) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
              --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg \
              > "$OUT/bench_dist1.json" 2> "$OUT/bench_dist1.err" ;;
@@ -58,6 +67,7 @@ run_stage() {
     *) echo "unknown stage $1"; return 2 ;;
   esac
 }
+trap 'du -sh "$OUT" 2>/dev/null' EXIT
 for s in "$@"; do
   echo "[gpu_run $(date +%T)] $s"
   run_stage "$s" || { rc=$?; echo "[gpu_run] stage $s failed rc=$rc"; exit $rc; }
