@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--dist-selftest", action="store_true",
                     help="initialise an RCCL process group even at N=1 (exercises the collective path "
                          "and its graph capture on a one-GPU box)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r1_final_pmc_traffic.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r2_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
     return ap.parse_args()
