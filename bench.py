@@ -197,6 +197,13 @@ def kernel_work(name, a):
     if name == "group_points_grad":
         B, C, N, S, K = a[2], a[3], a[4], a[5], a[6]
         return float(4 * B * C * N + 4 * B * S * K + 8 * B * C * S * K), "GB/s", HBM_PEAK, "hbm"
+    if name == "sa_group":       # xyz, new_xyz, points_t, idx, B, N, S, K, C, out, odt: per output row read
+        B, S, K, C, odt = a[4], a[6], a[7], a[8], a[10]   # the index, 12 B of xyz + 4C of points, write 3+C
+        rows = B * S * K
+        return float(rows * (4 + 12 + 4 * C + (3 + C) * es(odt)) + 12 * B * S), "GB/s", HBM_PEAK, "hbm"
+    if name == "sa_group_grad":  # g, gdt, idx, B, N, S, K, C, gp: zero gp, read g[..., 3:] + idx, scatter-add
+        gdt, B, N, S, K, C = a[1], a[3], a[4], a[5], a[6], a[7]
+        return float(4 * B * N * C + B * S * K * (4 + C * (es(gdt) + 4))), "GB/s", HBM_PEAK, "hbm"
     if name == "chamfer_3D.backward":  # xyz1, xyz2, B, n, m: per point read xyz, partner xyz, grad, idx; write own
         B, n, m = a[2], a[3], a[4]       # grad, scatter-add the partner's (12 + 12 + 4 + 4 + 12 + 12 B)
         return float(56 * B * (n + m)), "GB/s", HBM_PEAK, "hbm"
@@ -221,7 +228,8 @@ _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_d
             "gather_points": "gather_kernel", "gather_points_grad": "gather_grad_kernel",
             "group_points": "group_kernel", "group_points_grad": "group_grad_kernel",
             "chamfer_3D.backward": "chamfer_grad", "points2depth": "depth_", "points2grid": "points2grid",
-            "grid2image": "grid2image|image_normalize"}
+            "grid2image": "grid2image|image_normalize", "sa_group": "sa_group_kernel",
+            "sa_group_grad": "sa_group_grad_kernel"}
 
 
 def pmc_traffic(path, key, name):

@@ -68,6 +68,21 @@ int pcops_group_points(const float *points, const int *idx, int B, int C, int N,
 int pcops_group_points_grad(const float *grad_out, const int *idx, int B, int C, int N, int S, int K,
                             float *grad_points, pcops_stream_t stream);
 
+/* Fused SA-module grouping: sample_and_group_knn (models/model_utils.py:323-356)
+ * from the kNN indices onward, written in the channels_last layout the first
+ * 1x1 conv reads.  xyz (B,N,3), new_xyz (B,S,3), points_t (B,N,C) token-major
+ * (NULL when C == 0), idx (B,S,K) -> out (B,S,K,3+C) row-major:
+ *   out[b,s,k,c<3]  = xyz[b,idx,c] - new_xyz[b,s,c]      (grouped_xyz - centre)
+ *   out[b,s,k,3+c]  = points_t[b,idx,c]                  (grouped points)
+ * out_dtype 0 = fp32, 1 = bf16 (rounded once).  Replaces group_points x 2,
+ * the repeat/subtract, torch.cat and the channels_last copy. */
+int pcops_sa_group(const float *xyz, const float *new_xyz, const float *points_t, const int *idx, int B, int N, int S,
+                   int K, int C, void *out, int out_dtype, pcops_stream_t stream);
+/* grad_points_t (B,N,C) fp32, overwritten: scatter-add of grad_out[..., 3:] by idx
+ * (group_points_gpu.cu:43-64, token-major).  grad_dtype 0 = fp32, 1 = bf16. */
+int pcops_sa_group_grad(const void *grad_out, int grad_dtype, const int *idx, int B, int N, int S, int K, int C,
+                        float *grad_points_t, pcops_stream_t stream);
+
 /* ball_query(new_xyz, xyz, radius, nsample): ball_query.cpp:8-32, ball_query_gpu.cu:9-54.
  * new_xyz (B,M,3), xyz (B,N,3) -> idx (B,M,nsample). */
 int pcops_ball_query(const float *new_xyz, const float *xyz, int B, int N, int M, float radius, int nsample, int *idx,

@@ -32,6 +32,8 @@ _SIGS = {
     "pcops_gather_points_grad": (I, [P, P, I, I, I, I, P, P]),
     "pcops_group_points": (I, [P, P, I, I, I, I, I, P, P]),
     "pcops_group_points_grad": (I, [P, P, I, I, I, I, I, P, P]),
+    "pcops_sa_group": (I, [P, P, P, P, I, I, I, I, I, P, I, P]),
+    "pcops_sa_group_grad": (I, [P, I, P, I, I, I, I, I, P, P]),
     "pcops_ball_query": (I, [P, P, I, I, I, F, I, P, P]),
     "pcops_three_nn": (I, [P, P, I, I, I, P, P, P]),
     "pcops_three_interpolate": (I, [P, P, P, I, I, I, I, P, P]),

@@ -2,14 +2,17 @@
 //
 // Forward: both directions in ONE launch (blockIdx.x splits dir 0 = xyz1->xyz2
 // and dir 1 = xyz2->xyz1), each thread owning Q queries in VGPRs and the
-// target cloud streamed through a 1024-point LDS tile read by broadcast
-// ds_read_b128.  Per (query, target) pair the VALU does the reference's
-// direct-difference distance (3 sub + mul + 2 fma, nvcc contraction order)
-// and ONE v_min; the argmin is recovered per 32-target sub-tile (cmp +
-// 2 cndmask amortised over 32 pairs) and finally re-derived exactly from the
-// winning sub-tile.  Result: the reference's distance bits and its
-// lowest-index tie rule (strict '<' inside a chunk, strict '>' across
-// chunks, chamfer3D.cu:36,126) at 7 VALU ops / pair instead of 9.
+// target cloud streamed through a 1024-point LDS tile read by broadcast.
+// Two kernels, the same results (the reference's distance bits and its
+// lowest-index tie rule: strict '<' inside a chunk, strict '>' across chunks,
+// chamfer3D.cu:36,126):
+//   chamfer_nn_kernel      the reference's direct-difference distance per pair
+//                          (3 sub + mul + 2 fma, nvcc contraction order) and one
+//                          v_min; argmin recovered per 32-target sub-tile and
+//                          re-derived from the winning sub-tile (7 VALU / pair);
+//   chamfer_screen_kernel  ranks targets by |t|^2 - 2 a.t (3.5 VALU / pair) under
+//                          a rigorous rounding margin and re-derives the winner
+//                          with the direct expression (see its comment).
 //
 // Backward: own-point terms with plain stores, partner terms with float
 // atomics (the reference uses atomics for both, chamfer3D.cu:155-174).
@@ -354,11 +357,11 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
   auto blocks = [&](int q) {
     return (long)B * (((N + kThreads * q - 1) / (kThreads * q)) + ((M + kThreads * q - 1) / (kThreads * q)));
   };
-  int Q = 1;
-  if (blocks(4) >= 1024)
-    Q = 4;
-  else if (blocks(2) >= 512)
-    Q = 2;
+  // measured at B = 32 (tools/gpu_ab_chamfer.sh): the screened kernel wins at
+  // every step shape; 4 queries per lane once the grid holds >= 4 blocks per CU
+  // (16384^2: 1.55 ms vs 2.06 with Q = 1), 1 below that (2048^2: 0.070 ms vs
+  // 0.102 with Q = 2 and 0.172 for the direct kernel)
+  int Q = blocks(4) >= 1024 ? 4 : 1;
   if (const char *e = getenv("PCOPS_CHAMFER_Q")) Q = atoi(e);  // A/B experiments: 1, 2, 4, 8
   const int b0 = (N + kThreads * Q - 1) / (kThreads * Q);
   const int b1 = (M + kThreads * Q - 1) / (kThreads * Q);
@@ -372,6 +375,9 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
                        idx2, b0);
   else if (screen && Q == 2)
     hipLaunchKernelGGL(chamfer_screen_kernel<2>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1,
+                       idx2, b0);
+  else if (screen && Q == 1)
+    hipLaunchKernelGGL(chamfer_screen_kernel<1>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1,
                        idx2, b0);
   else if (Q == 8)
     hipLaunchKernelGGL(chamfer_nn_kernel<8>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1, idx2,

@@ -142,7 +142,83 @@ __global__ void three_interp_grad_kernel(const float *__restrict__ grad_out, con
   }
 }
 
+// ---- fused SA-module grouping (models/model_utils.py:323-356 sample_and_group_knn
+// + the channels_last copy the first 1x1 conv reads).  One thread per output
+// element of the (B, S, K, Ct) row-major tensor, Ct = 3 + C: channel c < 3 is
+// xyz[idx] - new_xyz (the reference's grouped_xyz -= new_xyz, fp32), channel
+// c >= 3 is points_t[b, idx, c - 3] (token-major points: a row copies C
+// contiguous floats).  Replaces two grouping launches, the repeat + subtract,
+// the channel concat and the NCHW -> channels_last copy (and, under autocast,
+// the bf16 cast: out_dtype 1 rounds once, as the cast would).
+__global__ void sa_group_kernel(const float *__restrict__ xyz, const float *__restrict__ new_xyz,
+                                const float *__restrict__ pts, const int *__restrict__ idx, int N, int S, int K,
+                                int C, int Ct, size_t total, void *__restrict__ out, int out_dt) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % Ct);
+    const size_t row = e / Ct;            // (b, s, k)
+    const size_t bs = row / K;            // (b, s)
+    const size_t b = bs / S;
+    const int a = idx[row];
+    const bool ok = (unsigned)a < (unsigned)N;
+    float v;
+    if (c < 3)
+      v = (ok ? xyz[(b * N + a) * 3 + c] : 0.f) - new_xyz[bs * 3 + c];
+    else
+      v = ok ? pts[(b * N + a) * C + (c - 3)] : 0.f;
+    if (out_dt == 1)
+      reinterpret_cast<__bf16 *>(out)[e] = (__bf16)v;
+    else
+      reinterpret_cast<float *>(out)[e] = v;
+  }
+}
+
+// grad_points_t[b, idx, c] += grad_out[b, s, k, 3 + c] (the group_points_grad
+// scatter-add, token-major; consecutive threads add to consecutive channels of
+// one row, so the atomics coalesce)
+__global__ void sa_group_grad_kernel(const void *__restrict__ g, int g_dt, const int *__restrict__ idx, int N, int S,
+                                     int K, int C, int Ct, size_t total, float *__restrict__ gpts) {
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const size_t row = e / C;
+    const size_t b = row / ((size_t)S * K);
+    const int a = idx[row];
+    if ((unsigned)a >= (unsigned)N) continue;
+    const size_t src = row * Ct + 3 + c;
+    const float v = g_dt == 1 ? (float)reinterpret_cast<const __bf16 *>(g)[src] : reinterpret_cast<const float *>(g)[src];
+    atomicAdd(gpts + (b * N + a) * C + c, v);
+  }
+}
+
 }  // namespace
+
+extern "C" int pcops_sa_group(const float *xyz, const float *new_xyz, const float *points_t, const int *idx, int B,
+                              int N, int S, int K, int C, void *out, int out_dtype, pcops_stream_t stream) {
+  if (B < 0 || N < 0 || S < 0 || K < 0 || C < 0 || (out_dtype != 0 && out_dtype != 1)) return PCOPS_ERR_INVALID;
+  const int Ct = 3 + C;
+  const size_t total = (size_t)B * S * K * Ct;
+  if (total == 0) return PCOPS_OK;
+  if (!xyz || !new_xyz || !idx || !out || (C > 0 && !points_t)) return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(sa_group_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, xyz, new_xyz,
+                     points_t, idx, N, S, K, C, Ct, total, out, out_dtype);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_sa_group_grad(const void *grad_out, int grad_dtype, const int *idx, int B, int N, int S, int K,
+                                   int C, float *grad_points_t, pcops_stream_t stream) {
+  if (B < 0 || N < 0 || S < 0 || K < 0 || C < 0 || (grad_dtype != 0 && grad_dtype != 1)) return PCOPS_ERR_INVALID;
+  if ((size_t)B * N * C == 0) return PCOPS_OK;
+  if (!grad_points_t) return PCOPS_ERR_INVALID;
+  if (hipMemsetAsync(grad_points_t, 0, sizeof(float) * (size_t)B * N * C, (hipStream_t)stream) != hipSuccess)
+    return PCOPS_ERR_LAUNCH;
+  const size_t total = (size_t)B * S * K * C;
+  if (total == 0) return PCOPS_OK;
+  if (!grad_out || !idx) return PCOPS_ERR_INVALID;
+  hipLaunchKernelGGL(sa_group_grad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, grad_out,
+                     grad_dtype, idx, N, S, K, C, 3 + C, total, grad_points_t);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
 
 extern "C" int pcops_group_points(const float *points, const int *idx, int B, int C, int N, int S, int K, float *out,
                                   pcops_stream_t stream) {

@@ -8,6 +8,7 @@ its model classes can import them unchanged:
   index_points(points, idx)                             :828-845
   fps_subsample(pcd, n_points=2048)                     :489-499
   sample_and_group_knn(xyz, points, npoint, k, ...)     :323-356
+  sample_and_group_knn_cl (fused grouping, channels_last) :323-356 + the first conv's layout
   self_attention / cross_attention / SDG_Decoder        :542-629
   self_attention_woinp / SDG_Decoder_PointSea           models_PointSea/model_utils.py:463-509
   PCViews                                               :1179-1234
@@ -74,6 +75,54 @@ def fps_subsample(pcd, n_points=2048):
     """pcd (B,N,3) -> (B,n_points,3) (model_utils.py:489-499)."""
     new_pcd = gather_operation(pcd.permute(0, 2, 1).contiguous(), furthest_point_sample(pcd.contiguous(), n_points))
     return new_pcd.permute(0, 2, 1).contiguous()
+
+
+class _SAGroup(torch.autograd.Function):
+    """pcops_sa_group: grouped (xyz - centre, points) rows in channels_last order."""
+
+    @staticmethod
+    def forward(ctx, xyz_t, new_xyz_t, points_t, idx, out_dtype):
+        B, N, _ = xyz_t.shape
+        S, K = idx.shape[1], idx.shape[2]
+        C = 0 if points_t is None else points_t.shape[2]
+        out = torch.empty(B, S, K, 3 + C, dtype=out_dtype, device=xyz_t.device)
+        with torch.cuda.device(xyz_t.device):
+            call("sa_group", lib().pcops_sa_group, ptr(xyz_t), ptr(new_xyz_t), ptr(points_t), ptr(idx), B, N, S, K, C,
+                 ptr(out), 1 if out_dtype == torch.bfloat16 else 0, stream_of(xyz_t))
+        ctx.save_for_backward(idx)
+        ctx.dims = (B, N, S, K, C)
+        ctx.mark_non_differentiable(idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        B, N, S, K, C = ctx.dims
+        if C == 0 or not ctx.needs_input_grad[2]:
+            return None, None, None, None, None
+        g = g.contiguous()
+        gp = torch.empty(B, N, C, dtype=torch.float32, device=g.device)
+        with torch.cuda.device(g.device):
+            call("sa_group_grad", lib().pcops_sa_group_grad, ptr(g), 1 if g.dtype == torch.bfloat16 else 0, ptr(idx),
+                 B, N, S, K, C, ptr(gp), stream_of(g))
+        return None, None, gp, None, None
+
+
+def sample_and_group_knn_cl(xyz, points_t, npoint, k, out_dtype=torch.float32):
+    """sample_and_group_knn (model_utils.py:323-356, use_xyz) in three launches --
+    FPS, kNN, and ONE fused grouping (pcops_sa_group) that writes the
+    neighbourhood features straight into the channels_last memory the first
+    1x1 conv reads.  xyz (B,3,N) without gradient, points_t (B,N,C) token-major
+    (or None) -> new_xyz (B,3,S), features (B,3+C,S,K) channels_last, idx."""
+    xyz_t = xyz.transpose(1, 2).contiguous()
+    fidx = furthest_point_sample(xyz_t, npoint)
+    new_xyz = gather_operation(xyz.contiguous(), fidx)                 # (B,3,S), the reference's new_xyz
+    new_xyz_t = new_xyz.transpose(1, 2).contiguous()
+    idx = query_knn(k, xyz_t, new_xyz_t)
+    if points_t is not None:
+        points_t = points_t.float().contiguous()
+    feat = _SAGroup.apply(xyz_t, new_xyz_t, points_t, idx, out_dtype)  # (B,S,K,3+C)
+    return new_xyz, feat.permute(0, 3, 1, 2), idx
 
 
 def sample_and_group_knn(xyz, points, npoint, k, use_xyz=True, idx=None):

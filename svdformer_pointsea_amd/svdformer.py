@@ -21,7 +21,7 @@ from torch import nn
 
 from .attention import SDG_Decoder, block_sum, cross_attention, linear, self_attention, to_channels, to_tokens
 from .chamfer3D import chamfer_3DDist
-from .model_utils import fps_subsample, group_local, sample_and_group_knn
+from .model_utils import fps_subsample, group_local, sample_and_group_knn, sample_and_group_knn_cl
 from ._lib import fork
 from .pointnet2_utils import furthest_point_sample, gather_operation
 
@@ -43,6 +43,16 @@ def max_over_neighbours(x):
 
 
 import os as _os
+
+# PCOPS_SA_FUSED=0: the unfused sample_and_group_knn path (A/B runs, parity tests)
+_SA_FUSED = _os.environ.get("PCOPS_SA_FUSED", "1") != "0"
+
+
+def max_over_neighbours_tokens(x):
+    """max over K of a (B, C, S, K) channels_last tensor, returned as (B, S, C)."""
+    if x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last):
+        return torch.max(x.permute(0, 2, 3, 1), dim=2)[0]
+    return torch.max(x, 3)[0].transpose(1, 2)
 
 # Which 1x1 convs run as GEMMs (A/B switch): sa | all (default) | edge | off.
 # The local encoder's EdgeConvs run on a side stream (Model.forward); their
@@ -220,7 +230,16 @@ class PointNet_SA_Module_KNN(nn.Module):
         self.pcsa = PCSA(mlp[-1], nsample) if (not group_all and use_pcsa) else None
 
     def forward(self, xyz, points, idx=None):
-        if self.group_all:
+        fused = (_SA_FUSED and not self.group_all and self.use_xyz and idx is None and xyz.is_cuda
+                 and not xyz.requires_grad and points is not None)
+        if fused:
+            # FPS -> kNN -> ONE grouping launch into the conv's channels_last input
+            # (model_utils.sample_and_group_knn_cl); points arrive token-major when
+            # they come from the previous SA module (its output is a (B,S,C) view)
+            dt = torch.bfloat16 if torch.is_autocast_enabled("cuda") else torch.float32
+            new_xyz, new_points, idx = sample_and_group_knn_cl(xyz, points.transpose(1, 2), self.npoint,
+                                                               self.nsample, dt)
+        elif self.group_all:
             new_xyz, new_points, idx, _ = sample_and_group_all(xyz, points, self.use_xyz)
         else:
             new_xyz, new_points, idx, _ = sample_and_group_knn(xyz, points, self.npoint, self.nsample, self.use_xyz,
@@ -228,7 +247,11 @@ class PointNet_SA_Module_KNN(nn.Module):
         new_points = self.mlp_conv(new_points.contiguous(memory_format=torch.channels_last))
         if self.pcsa is not None:
             new_points = self.pcsa(new_points)
-        new_points = max_over_neighbours(new_points)
+        if fused:
+            # (B,C,S) as a view of the (B,S,C) maximum: the next SA module reads it token-major
+            new_points = max_over_neighbours_tokens(new_points).transpose(1, 2)
+        else:
+            new_points = max_over_neighbours(new_points)
         return (new_xyz, new_points, idx) if self.if_idx else (new_xyz, new_points)
 
 
