@@ -375,6 +375,10 @@ __global__ __launch_bounds__(kThreads) void attn_dkv_kernel(const T *__restrict_
 // is on the matrix cores; one barrier per tile.  Half-wave exchange by
 // v_permlane32_swap; the softmax scale folded into the exp2 argument (fma).
 constexpr int kKT = 64;  // keys per tile
+#ifndef PCOPS_SCHED_DS
+#define PCOPS_SCHED_DS 1
+#endif
+constexpr bool kSchedDs = PCOPS_SCHED_DS;  // 0: compiler's own LDS/MFMA order (A/B builds)
 #ifndef PCOPS_DEFER_LOG2
 #define PCOPS_DEFER_LOG2 8.f  // 0 = rescale on every max increase (A/B builds)
 #endif
@@ -449,6 +453,38 @@ __device__ __forceinline__ void k_product(f32x16 &acc, const __bf16 *lds, const 
     const bf16x8 a = *reinterpret_cast<const bf16x8 *>(lds + img_off<D>(row, 2 * s + h));
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, f[s], acc, 0, 0, 0);
   }
+}
+
+// two independent chains interleaved (acc0 over lds0 . f0, acc1 over lds1 . f1):
+// consecutive MFMAs never wait on each other; each accumulator's order is
+// k_product's
+template <int D>
+__device__ __forceinline__ void k_product2(f32x16 &acc0, const __bf16 *lds0, const bf16x8 (&f0)[D / 16],
+                                           f32x16 &acc1, const __bf16 *lds1, const bf16x8 (&f1)[D / 16]) {
+  const int l = lane_(), h = l >> 5, row = l & 31;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8 *>(lds0 + img_off<D>(row, 2 * s + h));
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(lds1 + img_off<D>(row, 2 * s + h));
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, f0[s], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, f1[s], acc1, 0, 0, 0);
+  }
+}
+
+// Scheduling shape of an LDS-fed MFMA sequence of N MFMAs with R ds_reads
+// each: the first A MFMAs' reads go out first, then every MFMA is followed by
+// the reads of the MFMA A places later -- each read has A MFMAs (>= 64
+// cycles) to land instead of the compiler's read-wait-MFMA (lgkmcnt(0)
+// before every MFMA: the LDS latency exposed once per MFMA).
+template <int N, int R, int A>
+__device__ __forceinline__ void sched_ds_mfma() {
+  __builtin_amdgcn_sched_group_barrier(0x100, A * R, 0);
+#pragma unroll
+  for (int i = 0; i < N - A; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, A, 0);
 }
 
 // Y[db] += Rows^T(D x 32, Img<D> tile) . X   (X = fp32 accumulator of 32 rows)
@@ -533,8 +569,8 @@ __device__ __forceinline__ void fwd2_store(__bf16 *sk, __bf16 *sv, const typenam
   }
 }
 
-template <int D, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
+template <int D, int NW, int OCC>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void attn_fwd2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
                                                             const __bf16 *__restrict__ V, __bf16 *__restrict__ O,
                                                             float *__restrict__ lse, int Lq, int Lk, float scale,
                                                             Strides st) {
@@ -575,8 +611,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
     f32x16 X0 = f32x16{}, X1 = f32x16{};
-    k_product<D>(X0, ck, qf);
-    k_product<D>(X1, ck + 32 * C::kKS, qf);
+    k_product2<D>(X0, ck, qf, X1, ck + 32 * C::kKS, qf);
+    if constexpr (kSchedDs) sched_ds_mfma<D / 8, 1, 2>();
     if constexpr (EDGE) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -611,6 +647,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
     }
     v_product<D>(Y, cv, X0);
     v_product<D>(Y, cv + 32 * C::kVS, X1);
+    if constexpr (kSchedDs) sched_ds_mfma<D / 8, 2, (OCC >= 4 ? 1 : 2)>();
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   };
@@ -621,18 +658,36 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd2_kernel(const __bf16 *__rest
   if (h == 0 && qi < Lq && lse) lse[(long long)bh * Lq + qi] = (m + log2f(lsum)) * kLn2;
 }
 
-template <int D, int NW>
-int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, float scale,
-                const Strides &st, hipStream_t s) {
+int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+template <int D, int NW, int OCC>
+int launch_fwd2_occ(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk,
+                    float scale, const Strides &st, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_fwd2_kernel<D, NW>,
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_fwd2_kernel<D, NW, OCC>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_fwd2_kernel<D, NW>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+  hipLaunchKernelGGL((attn_fwd2_kernel<D, NW, OCC>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
                      (const __bf16 *)k, (const __bf16 *)v, (__bf16 *)o, lse, Lq, Lk, scale, st);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
+}
+
+// Occupancy: 8-wave blocks at <= 128 VGPRs run 2 blocks per CU instead of
+// one (130 -> 128 for D = 64: 0.466 -> 0.379 ms at (2048, 2048, B*H = 256)).
+// D = 128 needs ~200 (Y alone is 64).  PCOPS_FWD_OCC=1 lifts the cap (A/B).
+template <int D, int NW>
+int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, float scale,
+                const Strides &st, hipStream_t s) {
+  static const int occ = env_int("PCOPS_FWD_OCC", 4);
+  if constexpr (D <= 64 && NW == 8) {
+    if (occ == 4) return launch_fwd2_occ<D, NW, 4>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+  }
+  return launch_fwd2_occ<D, NW, 1>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
 }
 
 // ----------------------------------------------------------------- backward, bf16 (v2)

@@ -61,6 +61,19 @@ run_stage() {
     dist1) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
              --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg \
              > "$OUT/bench_dist1.json" 2> "$OUT/bench_dist1.err" ;;
+    pmc_attn2)
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_MISC \
+        --kernel-include-regex 'attn_' --output-format csv -d "$OUT/pmc_attn2" -o run -- \
+        python tools/attn_bench.py 0 1 > "$OUT/pmc_attn2.log" 2>&1 &&
+      python tools/pmc_summary.py "$(find "$OUT/pmc_attn2" -name '*counter_collection.csv' -print -quit)" \
+        > "$OUT/pmc_attn2_summary.txt" ;;
+    attn_ab)   # A/B of attention variants selected by env (ATTN_AB="VAR=a VAR=b;VAR=c" groups)
+      IFS=';' read -ra groups <<< "${ATTN_AB:-PCOPS_FWD_PIPE=0}"
+      for g in "${groups[@]}"; do
+        echo "== $g" >> "$OUT/attn_ab.txt"
+        env $g timeout -k 10 120 python tools/attn_bench.py ${ATTN_SHAPES:-0 1 2 3} >> "$OUT/attn_ab.txt" 2>&1 || return 1
+      done ;;
     avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
     knn) timeout -k 10 120 python tools/knn_bench.py > "$OUT/knn_bench.txt" 2>&1 ;;
     chamfer) timeout -k 10 120 python tools/microbench.py > "$OUT/chamfer_bench.txt" 2>&1 ;;
