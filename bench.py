@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-leg", action="store_true",
                     help="skip the configs[1] figure (fp32 forward + loss, B=16) reported beside the bf16 step")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="issue every launch from Python (no HIP graph)")
     ap.add_argument("--timing-steps", type=int, default=2, help="eager steps timed per launch (graph mode)")
@@ -353,14 +353,28 @@ def cpu_baseline(wl, steps):
 
     with cpu_ops():
         step()  # warm-up
-        t0 = time.perf_counter()
+        times = []
         for _ in range(steps):
+            t0 = time.perf_counter()
             step()
-        dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "samples/s", "cores": nthreads, "kind": "port",
-            "sample": f"{steps} train steps of 1 {wl.name} sample (2048->{wl.n_out}) after 1 warm-up, fp32: "
-                      f"torch CPU ({nthreads} threads) + oracle/pcops_oracle.c point ops (1 thread) + torch CPU "
-                      f"attention"}
+            times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": 1.0 / med, "unit": "samples/s", "cores": nthreads, "kind": "port",
+            "cpu_model": _cpu_model(), "step_s": [round(t, 3) for t in times],
+            "sample": f"median of {steps} train steps of 1 {wl.name} sample (2048->{wl.n_out}) after 1 warm-up, "
+                      f"fp32: torch CPU ({nthreads} threads) + oracle/pcops_oracle.c point ops (OpenMP, "
+                      f"{nthreads} threads) + torch CPU attention"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 # ------------------------------------------------------------------ configs[1] leg

@@ -280,10 +280,12 @@ EXPORT void oracle_three_interpolate_grad(int B, int C, int N, int M, const floa
  * the nearest point of b (squared distance) and the LOWEST index among equal
  * minima (strict '<' inside a 512-chunk, strict '>' across chunks). */
 static void chamfer_dir(int B, int N, const float *a, int M, const float *bb, float *dist, int *idx) {
+  /* every (b, j) output is independent: OpenMP over them changes no result */
+#pragma omp parallel for collapse(2) schedule(static)
   for (int b = 0; b < B; ++b) {
-    const float *pa = a + (size_t)b * N * 3;
-    const float *pb = bb + (size_t)b * M * 3;
     for (int j = 0; j < N; ++j) {
+      const float *pa = a + (size_t)b * N * 3;
+      const float *pb = bb + (size_t)b * M * 3;
       const float x1 = pa[3 * j], y1 = pa[3 * j + 1], z1 = pa[3 * j + 2];
       float best = 0.f;
       int besti = 0;
@@ -382,13 +384,17 @@ EXPORT float oracle_torch_sumsq(const float *v, int C, int stride) {
  * (query_knn include_self=False -> pad 1). */
 EXPORT void oracle_knn(int B, int S, int N, int C, int K, int pad, const float *q, const float *p, int *idx,
                        float *dist) {
-  float *d = (float *)malloc(sizeof(float) * (size_t)N);
-  int *order = (int *)malloc(sizeof(int) * (size_t)N);
   float *pn = (float *)malloc(sizeof(float) * (size_t)N);
   for (int b = 0; b < B; ++b) {
     const float *qb = q + (size_t)b * S * C;
     const float *pb = p + (size_t)b * N * C;
     for (int n = 0; n < N; ++n) pn[n] = oracle_torch_sumsq(pb + (size_t)n * C, C, 1);
+    /* queries are independent: OpenMP over them changes no result */
+#pragma omp parallel
+    {
+    float *d = (float *)malloc(sizeof(float) * (size_t)N);
+    int *order = (int *)malloc(sizeof(int) * (size_t)N);
+#pragma omp for schedule(static)
     for (int s = 0; s < S; ++s) {
       const float *qq = qb + (size_t)s * C;
       const float qn = oracle_torch_sumsq(qq, C, 1);
@@ -416,9 +422,10 @@ EXPORT void oracle_knn(int B, int S, int N, int C, int K, int pad, const float *
         if (dist) dist[((size_t)b * S + s) * K + k] = (k + pad < cnt) ? d[o] : 0.f;
       }
     }
+    free(d);
+    free(order);
+    }
   }
-  free(d);
-  free(order);
   free(pn);
 }
 

@@ -697,7 +697,7 @@ int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse
 // hold the two halves of the row: one permlane32 swap adds them) and written
 // to delta_out for the dK/dV pass -- no separate preprocess launch, no second
 // read of dO.
-template <int D, int NW, int OCC, bool FD>
+template <int D, int NW, int OCC, bool FD, bool HS>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dq2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
                                                            const __bf16 *__restrict__ V, const __bf16 *__restrict__ dO,
                                                            const float *__restrict__ lse,
@@ -758,24 +758,44 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
     if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
-    f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
-    k_product<D>(S0, ck, qf);
-    k_product<D>(S1, ck + 32 * C::kKS, qf);
-    k_product<D>(G0, cv, gf);
-    k_product<D>(G1, cv + 32 * C::kVS, gf);
+    if constexpr (HS) {
+      // one 32-key half at a time: half the live S / dP registers (the
+      // accumulation order of Y is unchanged)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float p0 = exp2_ftz(__builtin_fmaf(S0[r], sl2, -lse2));
-      float p1 = exp2_ftz(__builtin_fmaf(S1[r], sl2, -lse2));
-      if constexpr (EDGE) {
-        if (k0 + acc_row(r, h) >= Lk) p0 = 0.f;
-        if (k0 + 32 + acc_row(r, h) >= Lk) p1 = 0.f;
+      for (int hf = 0; hf < 2; ++hf) {
+        f32x16 S = f32x16{}, G = f32x16{};
+        k_product<D>(S, ck + 32 * hf * C::kKS, qf);
+        k_product<D>(G, cv + 32 * hf * C::kVS, gf);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2_ftz(__builtin_fmaf(S[r], sl2, -lse2));
+          if constexpr (EDGE) {
+            if (k0 + 32 * hf + acc_row(r, h) >= Lk) p = 0.f;
+          }
+          S[r] = p * (G[r] - dl);  // dS^T without the softmax scale
+        }
+        v_product<D>(Y, ck + 32 * hf * C::kKS, S);
       }
-      S0[r] = p0 * (G0[r] - dl);  // dS^T without the softmax scale
-      S1[r] = p1 * (G1[r] - dl);
+    } else {
+      f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
+      k_product<D>(S0, ck, qf);
+      k_product<D>(S1, ck + 32 * C::kKS, qf);
+      k_product<D>(G0, cv, gf);
+      k_product<D>(G1, cv + 32 * C::kVS, gf);
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p0 = exp2_ftz(__builtin_fmaf(S0[r], sl2, -lse2));
+        float p1 = exp2_ftz(__builtin_fmaf(S1[r], sl2, -lse2));
+        if constexpr (EDGE) {
+          if (k0 + acc_row(r, h) >= Lk) p0 = 0.f;
+          if (k0 + 32 + acc_row(r, h) >= Lk) p1 = 0.f;
+        }
+        S0[r] = p0 * (G0[r] - dl);  // dS^T without the softmax scale
+        S1[r] = p1 * (G1[r] - dl);
+      }
+      v_product<D>(Y, ck, S0);
+      v_product<D>(Y, ck + 32 * C::kKS, S1);
     }
-    v_product<D>(Y, ck, S0);
-    v_product<D>(Y, ck + 32 * C::kKS, S1);
     if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   };
@@ -888,16 +908,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
       for (int hf = 0; hf < 2; ++hf) {
         f32x16 S = f32x16{}, G = f32x16{};
         k_product<D>(S, cq + 32 * hf * C::kKS, kf);
-        if (MODE == 2) k_product<D>(G, cg + 32 * hf * C::kVS, vf);
+        if (MODE != 1) k_product<D>(G, cg + 32 * hf * C::kVS, vf);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = acc_row(r, h) + 32 * hf;
           const float p = exp2_ftz(__builtin_fmaf(S[r], sl2, -cl[row]));
           S[r] = p;
-          if (MODE == 2) G[r] = p * (G[r] - cd[row]);
+          if (MODE != 1) G[r] = p * (G[r] - cd[row]);
         }
-        if (MODE == 1) v_product<D>(Y1, cg + 32 * hf * C::kVS, S);
-        if (MODE == 2) v_product<D>(Y2, cq + 32 * hf * C::kKS, G);
+        if (MODE != 2) v_product<D>(Y1, cg + 32 * hf * C::kVS, S);
+        if (MODE != 1) v_product<D>(Y2, cq + 32 * hf * C::kKS, G);
       }
     }
     if (t + 1 < ntiles) {
@@ -913,17 +933,27 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
   if (MODE != 1) store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
 }
 
+// D = 64 runs 4-wave blocks at 3 waves per SIMD (the key-half split fits
+// 162 VGPRs): three independent blocks per CU instead of one 8-wave block.
+// PCOPS_DQ_NW4=0 keeps the 8-wave form (A/B).
+template <int D, int NW>
+struct Dq2Cfg {
+  static constexpr bool kHS = D == 64 && NW == 4;
+  static constexpr int kOcc = kHS ? 3 : (D <= 96 || NW == 8) ? 2 : 1;
+};
+
 template <int D, int NW, bool FD>
 int launch_dq2_impl(const void *q, const void *k, const void *v, const void *dout, const float *lse,
                     const float *delta, void *dq, int BH, int Lq, int Lk, float scale, const Strides &st,
                     const void *o, float *delta_out, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
-  constexpr int OCC = (D <= 96 || NW == 8) ? 2 : 1;
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC, FD>,
+  constexpr int OCC = Dq2Cfg<D, NW>::kOcc;
+  constexpr bool HS = Dq2Cfg<D, NW>::kHS;
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC, FD, HS>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD, HS>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
                      (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dq, Lq, Lk,
                      scale, st, (const __bf16 *)o, delta_out);
   PC_CHECK_LAUNCH();
@@ -991,9 +1021,11 @@ int dq2_dispatch(const void *q, const void *k, const void *v, const void *dout, 
     case 32:
       return wide ? launch_dq2<32, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
                   : launch_dq2<32, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
-    case 64:
-      return wide ? launch_dq2<64, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
-                  : launch_dq2<64, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+    case 64: {
+      static const int nw4 = env_int("PCOPS_DQ_NW4", 1);
+      return (wide && !nw4) ? launch_dq2<64, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
+                            : launch_dq2<64, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+    }
     case 96:
       return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
     case 128:
