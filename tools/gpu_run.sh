@@ -14,6 +14,8 @@
 #   pmc_attn     SQ counter pass over the attention kernels (tools/attn_bench.py)
 #   dist1        bench.py under torch.distributed.run with ONE rank and an RCCL group
 #                (--dist-selftest): the bucketed all-reduce captured in the graph
+#   step_profile tools/step_profile.py (torch-profiler op/kernel breakdown of one eager step)
+#   attn_ab      tools/attn_bench.py once per env group in $ATTN_AB (A/B of attention variants)
 #   avail        rocprofv3 --list-avail
 #   knn          tools/knn_bench.py ; chamfer: tools/microbench.py chamfer
 set -o pipefail
@@ -74,6 +76,7 @@ run_stage() {
         echo "== $g" >> "$OUT/attn_ab.txt"
         env $g timeout -k 10 120 python tools/attn_bench.py ${ATTN_SHAPES:-0 1 2 3} >> "$OUT/attn_ab.txt" 2>&1 || return 1
       done ;;
+    step_profile) timeout -k 10 400 python tools/step_profile.py --rows 60 > "$OUT/step_ops.txt" 2>&1 ;;
     avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
     knn) timeout -k 10 120 python tools/knn_bench.py > "$OUT/knn_bench.txt" 2>&1 ;;
     chamfer) timeout -k 10 120 python tools/microbench.py > "$OUT/chamfer_bench.txt" 2>&1 ;;
