@@ -680,6 +680,8 @@ int launch_fwd2_occ(const void *q, const void *k, const void *v, void *o, float 
 // Occupancy: 8-wave blocks at <= 128 VGPRs run 2 blocks per CU instead of
 // one (130 -> 128 for D = 64: 0.466 -> 0.379 ms at (2048, 2048, B*H = 256)).
 // D = 128 needs ~200 (Y alone is 64).  PCOPS_FWD_OCC=1 lifts the cap (A/B).
+// 4-wave blocks (short sequences) are capped at 2 waves per SIMD: left
+// alone the compiler gives them 400+ registers (one wave per SIMD).
 template <int D, int NW>
 int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, float scale,
                 const Strides &st, hipStream_t s) {
@@ -687,7 +689,14 @@ int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse
   if constexpr (D <= 64 && NW == 8) {
     if (occ == 4) return launch_fwd2_occ<D, NW, 4>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
   }
-  return launch_fwd2_occ<D, NW, 1>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+  // D = 96 runs 4-wave blocks at any length (201 VGPRs: two independent
+  // blocks per CU beat one 8-wave block at 185, 512^2 0.052 -> 0.047 ms);
+  // D = 128 does not (2048^2 0.644 -> 0.719 ms)
+  if constexpr (NW == 4 || D == 96) {
+    return launch_fwd2_occ<D, 4, 2>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+  } else {
+    return launch_fwd2_occ<D, NW, 1>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+  }
 }
 
 // ----------------------------------------------------------------- backward, bf16 (v2)
@@ -938,8 +947,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
 // PCOPS_DQ_NW4=0 keeps the 8-wave form (A/B).
 template <int D, int NW>
 struct Dq2Cfg {
-  static constexpr bool kHS = D == 64 && NW == 4;
-  static constexpr int kOcc = kHS ? 3 : (D <= 96 || NW == 8) ? 2 : 1;
+  static constexpr bool kHS = (D == 64 || D == 128) && NW == 4;  // D = 128, NW = 4: short sequences only
+  static constexpr int kOcc = kHS ? (D == 64 ? 3 : 2) : (D <= 96 || NW == 8) ? 2 : 1;
 };
 
 template <int D, int NW, bool FD>
