@@ -66,14 +66,19 @@ __global__ __launch_bounds__(256) void transpose_add_kernel(const void *__restri
 // ---------------------------------------------------------------- LayerNorm
 // A row is read as 8-element chunks (one 16-B load for bf16, two for fp32);
 // chunk ch = lane + 64*i, so C <= 1024 needs at most 2 chunks per lane.
+// The operand configuration (dtypes, residual present, which upstream
+// gradients) is a template: with runtime dtype / presence tests hipcc split
+// every load into its own branch and waited for each one (vmcnt(0) six times
+// per row) -- the backward ran at 2.5 TB/s.  Now a row's loads issue together.
 constexpr int kMaxCh = 2;
 
 struct V8 {
   float v[8];
 };
 
-__device__ __forceinline__ void ld8(V8 &o, const void *p, int dt, long long e) {
-  if (dt == 0) {
+template <int DT>
+__device__ __forceinline__ void ld8c(V8 &o, const void *p, long long e) {
+  if constexpr (DT == 0) {
     const float4 x = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + e);
     const float4 y = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + e + 4);
     o.v[0] = x.x, o.v[1] = x.y, o.v[2] = x.z, o.v[3] = x.w, o.v[4] = y.x, o.v[5] = y.y, o.v[6] = y.z, o.v[7] = y.w;
@@ -96,8 +101,10 @@ __device__ __forceinline__ void st8_bf16(__bf16 *p, long long e, const V8 &o) {
   *reinterpret_cast<bf16x8_t *>(p + e) = x;
 }
 
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a, int adt, const void *__restrict__ b,
-                                                     int bdt, const float *__restrict__ gamma,
+// AT: a's dtype; BT: b's dtype or -1 (no residual)
+template <int CH, int AT, int BT>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a, const void *__restrict__ b,
+                                                     const float *__restrict__ gamma,
                                                      const float *__restrict__ beta, float eps, int rows, int C,
                                                      float *__restrict__ y32, __bf16 *__restrict__ y16,
                                                      float *__restrict__ mean_out, float *__restrict__ rstd_out) {
@@ -106,36 +113,42 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a,
   if (row >= rows) return;
   const int nch = C >> 3;
   const long long base = (long long)row * C;
-  V8 x[kMaxCh];
+  // every lane loads (chunk index clamped, no branches: the loads of both
+  // chunks and both operands issue back to back); lanes past the row end
+  // contribute zeros
+  V8 x[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int ch = min(lane + 64 * i, nch - 1);
+    ld8c<AT>(x[i], a, base + 8 * ch);
+    if constexpr (BT >= 0) {
+      V8 t;
+      ld8c<BT>(t, b, base + 8 * ch);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[i].v[k] += t.v[k];
+    }
+  }
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxCh; ++i) {
-    const int ch = lane + 64 * i;
-    if (ch < nch) {
-      ld8(x[i], a, adt, base + 8 * ch);
-      if (b) {
-        V8 t;
-        ld8(t, b, bdt, base + 8 * ch);
+  for (int i = 0; i < CH; ++i) {
+    const bool ok = lane + 64 * i < nch;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) x[i].v[k] += t.v[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s += x[i].v[k];
-    }
+    for (int k = 0; k < 8; ++k) s += ok ? x[i].v[k] : 0.f;
   }
   const float mean = wave_sum_f32(s) / (float)C;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxCh; ++i)
-    if (lane + 64 * i < nch)
+  for (int i = 0; i < CH; ++i) {
+    const bool ok = lane + 64 * i < nch;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float d = x[i].v[k] - mean;
-        q = __builtin_fmaf(d, d, q);
-      }
+    for (int k = 0; k < 8; ++k) {
+      const float d = ok ? x[i].v[k] - mean : 0.f;
+      q = __builtin_fmaf(d, d, q);
+    }
+  }
   const float rstd = 1.f / sqrtf(wave_sum_f32(q) / (float)C + eps);
 #pragma unroll
-  for (int i = 0; i < kMaxCh; ++i) {
+  for (int i = 0; i < CH; ++i) {
     const int ch = lane + 64 * i;
     if (ch < nch) {
       V8 y;
@@ -162,60 +175,61 @@ int ln_bwd_rpw(int rows) {
   return r < 4 ? 4 : (r > 16 ? 16 : r);
 }
 
-template <int CH>  // 8-element chunks per lane: 1 for C <= 512 (half the registers), 2 for C <= 1024
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g32, const __bf16 *__restrict__ g16,
-                                                     const void *__restrict__ a, int adt, const void *__restrict__ b,
-                                                     int bdt, const float *__restrict__ gamma,
-                                                     const float *__restrict__ mean_in,
-                                                     const float *__restrict__ rstd_in, int rows, int C,
-                                                     float *__restrict__ dx32, __bf16 *__restrict__ dx16,
-                                                     int rpw, float *__restrict__ part) {
+// CH: 8-element chunks per lane (1 for C <= 512, 2 for C <= 1024); AT / BT as
+// the forward; GM: which upstream gradients are present (1 = dy32, 2 = dy16, 3 both)
+template <int CH, int AT, int BT, int GM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4 : 3))) void ln_bwd_kernel(
+    const float *__restrict__ g32, const __bf16 *__restrict__ g16, const void *__restrict__ a,
+    const void *__restrict__ b, const float *__restrict__ gamma, const float *__restrict__ mean_in,
+    const float *__restrict__ rstd_in, int rows, int C, float *__restrict__ dx32, __bf16 *__restrict__ dx16, int rpw,
+    float *__restrict__ part) {
   extern __shared__ float ln_red[];  // [4][2C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = C >> 3;
-  V8 dg[CH], db[CH];
+  V8 dg[CH], db[CH], gm[CH];
 #pragma unroll
-  for (int i = 0; i < CH; ++i)
+  for (int i = 0; i < CH; ++i) {
+    ld8c<0>(gm[i], gamma, 8 * min(lane + 64 * i, nch - 1));  // hoisted out of the row loop
 #pragma unroll
     for (int k = 0; k < 8; ++k) dg[i].v[k] = db[i].v[k] = 0.f;
+  }
   const int r0 = (blockIdx.x * 4 + w) * rpw;
   for (int row = r0; row < r0 + rpw && row < rows; ++row) {
     const long long base = (long long)row * C;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    V8 xh[CH], dy[CH];
+    // all loads of the row first (clamped chunk index, no branches), then the
+    // arithmetic; lanes past the row end carry dy = xh = 0
+    V8 xh[CH], dy[CH], t[CH], u[CH], v[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const long long e = base + 8 * min(lane + 64 * i, nch - 1);
+      ld8c<AT>(xh[i], a, e);
+      if constexpr (BT >= 0) ld8c<BT>(t[i], b, e);
+      if constexpr (GM & 1) ld8c<0>(u[i], g32, e);
+      if constexpr (GM & 2) ld8c<1>(v[i], g16, e);
+    }
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      const int ch = lane + 64 * i;
-      if (ch < nch) {
-        V8 t;
-        ld8(xh[i], a, adt, base + 8 * ch);
-        if (b) {
-          ld8(t, b, bdt, base + 8 * ch);
+      const bool ok = lane + 64 * i < nch;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) xh[i].v[k] += t.v[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) dy[i].v[k] = 0.f;
-        if (g32) {
-          ld8(t, g32, 0, base + 8 * ch);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) dy[i].v[k] += t.v[k];
-        }
-        if (g16) {
-          ld8(t, g16, 1, base + 8 * ch);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) dy[i].v[k] += t.v[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          xh[i].v[k] = (xh[i].v[k] - mean) * rstd;
-          dg[i].v[k] = __builtin_fmaf(dy[i].v[k], xh[i].v[k], dg[i].v[k]);
-          db[i].v[k] += dy[i].v[k];
-          const float g = dy[i].v[k] * gamma[8 * ch + k];
-          sg += g;
-          sgx = __builtin_fmaf(g, xh[i].v[k], sgx);
-        }
+      for (int k = 0; k < 8; ++k) {
+        float x = xh[i].v[k];
+        if constexpr (BT >= 0) x += t[i].v[k];
+        float d;
+        if constexpr (GM == 3)
+          d = u[i].v[k] + v[i].v[k];
+        else if constexpr (GM == 1)
+          d = u[i].v[k];
+        else
+          d = v[i].v[k];
+        xh[i].v[k] = ok ? (x - mean) * rstd : 0.f;
+        dy[i].v[k] = ok ? d : 0.f;
+        dg[i].v[k] = __builtin_fmaf(dy[i].v[k], xh[i].v[k], dg[i].v[k]);
+        db[i].v[k] += dy[i].v[k];
+        const float g = dy[i].v[k] * gm[i].v[k];
+        sg += g;
+        sgx = __builtin_fmaf(g, xh[i].v[k], sgx);
       }
     }
     const float mg = wave_sum_f32(sg) / (float)C;
@@ -226,8 +240,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
       if (ch < nch) {
         V8 dx;
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          dx.v[k] = rstd * (dy[i].v[k] * gamma[8 * ch + k] - mg - xh[i].v[k] * mgx);
+        for (int k = 0; k < 8; ++k) dx.v[k] = rstd * (dy[i].v[k] * gm[i].v[k] - mg - xh[i].v[k] * mgx);
         if (dx32) st8_f32(dx32, base + 8 * ch, dx);
         if (dx16) st8_bf16(dx16, base + 8 * ch, dx);
       }
@@ -248,6 +261,75 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float *__restrict__ g
   for (int c = threadIdx.x; c < 2 * C; c += 256)
     pb[c] = ((ln_red[c] + ln_red[2 * C + c]) + ln_red[4 * C + c]) + ln_red[6 * C + c];
 }
+
+// ---- host dispatch over the operand configurations
+struct LnArgs {
+  const void *a, *b;
+  const float *g32;
+  const __bf16 *g16;
+  const float *gamma, *beta, *mean, *rstd;
+  float eps;
+  int rows, C;
+  float *y32;
+  __bf16 *y16;
+  float *part;
+  hipStream_t s;
+};
+
+template <int CH, int AT, int BT>
+void ln_fwd_go(const LnArgs &p) {
+  hipLaunchKernelGGL((ln_fwd_kernel<CH, AT, BT>), dim3((p.rows + 3) / 4), dim3(256), 0, p.s, p.a, p.b, p.gamma,
+                     p.beta, p.eps, p.rows, p.C, p.y32, p.y16, const_cast<float *>(p.mean),
+                     const_cast<float *>(p.rstd));
+}
+
+template <int CH, int AT, int BT, int GM>
+void ln_bwd_go(const LnArgs &p, int blocks, int rpw) {
+  hipLaunchKernelGGL((ln_bwd_kernel<CH, AT, BT, GM>), dim3(blocks), dim3(256), 4 * 2 * p.C * sizeof(float), p.s,
+                     p.g32, p.g16, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16, rpw, p.part);
+}
+
+// CH x AT x BT resolved at compile time from runtime codes (bt = -1: no b)
+template <template <int, int, int> class F, typename... A>
+void ln_dispatch(int ch, int at, int bt, A &&...args) {
+#define LN_BT(CH_, AT_)                                  \
+  if (bt < 0)                                            \
+    F<CH_, AT_, -1>::go(args...);                        \
+  else if (bt == 0)                                      \
+    F<CH_, AT_, 0>::go(args...);                         \
+  else                                                   \
+    F<CH_, AT_, 1>::go(args...);
+  if (ch == 1) {
+    if (at == 0) {
+      LN_BT(1, 0)
+    } else {
+      LN_BT(1, 1)
+    }
+  } else {
+    if (at == 0) {
+      LN_BT(2, 0)
+    } else {
+      LN_BT(2, 1)
+    }
+  }
+#undef LN_BT
+}
+
+template <int CH, int AT, int BT>
+struct LnFwdF {
+  static void go(const LnArgs &p) { ln_fwd_go<CH, AT, BT>(p); }
+};
+template <int CH, int AT, int BT>
+struct LnBwdF {
+  static void go(const LnArgs &p, int gm, int blocks, int rpw) {
+    if (gm == 3)
+      ln_bwd_go<CH, AT, BT, 3>(p, blocks, rpw);
+    else if (gm == 1)
+      ln_bwd_go<CH, AT, BT, 1>(p, blocks, rpw);
+    else
+      ln_bwd_go<CH, AT, BT, 2>(p, blocks, rpw);
+  }
+};
 
 int ln_bwd_blocks(int rows) {
   const int rpb = 4 * ln_bwd_rpw(rows);
@@ -284,7 +366,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restr
 #pragma unroll 16
   for (; r < r1; r += step) {
     V8 t;
-    ld8(t, g, DT, r * C + col);
+    ld8c<DT>(t, g, r * C + col);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] += t.v[k];
   }
@@ -375,8 +457,20 @@ extern "C" int pcops_layernorm_fwd(const void *a, int a_dtype, const void *b, in
   if (C > 512 * kMaxCh || C % 8) return PCOPS_ERR_UNSUPPORTED;
   if (!a || !gamma || !beta || !mean || !rstd || (!y32 && !y16) || !dt_ok(a_dtype) || (b && !dt_ok(b_dtype)))
     return PCOPS_ERR_INVALID;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, a, a_dtype, b, b_dtype,
-                     gamma, beta, eps, rows, C, y32, (__bf16 *)y16, mean, rstd);
+  LnArgs p{};
+  p.a = a;
+  p.b = b;
+  p.gamma = gamma;
+  p.beta = beta;
+  p.mean = mean;
+  p.rstd = rstd;
+  p.eps = eps;
+  p.rows = rows;
+  p.C = C;
+  p.y32 = y32;
+  p.y16 = (__bf16 *)y16;
+  p.s = (hipStream_t)stream;
+  ln_dispatch<LnFwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
@@ -406,18 +500,22 @@ extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const vo
   if (!workspace || workspace_bytes < pcops_layernorm_bwd_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
   const int blocks = ln_bwd_blocks(rows);
   float *part = (float *)workspace;
-  static const bool force2 = [] {  // A/B: PCOPS_LN_CH2=1 runs every C on the two-chunk kernel
-    const char *e = getenv("PCOPS_LN_CH2");
-    return e && e[0] == '1';
-  }();
-  if (C <= 512 && !force2)
-    hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(blocks), dim3(256), 4 * 2 * C * sizeof(float), s, dy32,
-                       (const __bf16 *)dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16,
-                       ln_bwd_rpw(rows), part);
-  else
-    hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(blocks), dim3(256), 4 * 2 * C * sizeof(float), s, dy32,
-                       (const __bf16 *)dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, (__bf16 *)dx16,
-                       ln_bwd_rpw(rows), part);
+  LnArgs p{};
+  p.a = a;
+  p.b = b;
+  p.g32 = dy32;
+  p.g16 = (const __bf16 *)dy16;
+  p.gamma = gamma;
+  p.mean = mean;
+  p.rstd = rstd;
+  p.rows = rows;
+  p.C = C;
+  p.y32 = dx32;
+  p.y16 = (__bf16 *)dx16;
+  p.part = part;
+  p.s = s;
+  ln_dispatch<LnBwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p, (dy32 ? 1 : 0) | (dy16 ? 2 : 0), blocks,
+                      ln_bwd_rpw(rows));
   hipLaunchKernelGGL(colsum_final_kernel, dim3((2 * C + 31) / 32), dim3(1024), 0, s, part, blocks, 2 * C,
                      (void *)dgamma, 0, C, (void *)dbeta);
   PC_CHECK_LAUNCH();

@@ -249,6 +249,45 @@ def test_layernorm_and_transpose_kernels(dev, B, L, C):
     torch.testing.assert_close(z.float(), (x + x.to(torch.bfloat16).float()).to(torch.bfloat16).float())
 
 
+@pytest.mark.parametrize("adt,bdt", [(torch.float32, None), (torch.bfloat16, None), (torch.bfloat16, torch.float32),
+                                     (torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize("C", [96, 512, 768, 1024])
+def test_layernorm_operand_configs(dev, adt, bdt, C):
+    """Every compiled operand configuration of pcops_layernorm_fwd/bwd (a / b
+    dtypes, residual or not, both output copies with gradients on both), at a
+    full-lane C (512, 1024) and partial-chunk C (96, 768), against torch."""
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(C)
+    rows = 999
+    norm = torch.nn.LayerNorm(C).to(dev)
+    with torch.no_grad():
+        norm.weight.normal_()
+        norm.bias.normal_()
+    a = torch.randn(rows, C, device=dev).to(adt).requires_grad_(True)
+    b = None if bdt is None else torch.randn(rows, C, device=dev).to(bdt).requires_grad_(True)
+    y32, y16 = A._LayerNorm.apply(a, b, norm.weight, norm.bias, norm.eps, True)
+    x = a.float() + (0 if b is None else b.float())
+    ref = torch.nn.functional.layer_norm(x, (C,), norm.weight, norm.bias, norm.eps)
+    torch.testing.assert_close(y32, ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(y16, y32.to(torch.bfloat16))
+    g1, g2 = torch.randn_like(y32), torch.randn_like(y32).to(torch.bfloat16)
+    torch.autograd.backward([y32, y16], [g1, g2])
+    xr = x.detach().requires_grad_(True)
+    w = norm.weight.detach().clone().requires_grad_(True)
+    bb = norm.bias.detach().clone().requires_grad_(True)
+    (torch.nn.functional.layer_norm(xr, (C,), w, bb, norm.eps) * (g1 + g2.float())).sum().backward()
+    tol = dict(rtol=1e-4, atol=1e-5) if adt == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    assert a.grad.dtype == adt
+    torch.testing.assert_close(a.grad.float(), xr.grad.to(adt).float(), **tol)
+    if b is not None:
+        assert b.grad.dtype == bdt
+        torch.testing.assert_close(b.grad.float(), xr.grad.to(bdt).float(),
+                                   **(dict(rtol=1e-4, atol=1e-5) if bdt == torch.float32 else dict(rtol=1e-2, atol=1e-2)))
+    torch.testing.assert_close(norm.weight.grad, w.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(norm.bias.grad, bb.grad, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("amp", [False, True])
 @pytest.mark.parametrize("cin,cout,T", [(40, 8, 999), (512, 512, 65536), (64, 3072, 16384)])
 def test_linear_splitk_wgrad(dev, amp, cin, cout, T):
