@@ -23,11 +23,14 @@ def _free_port():
 
 @pytest.fixture(scope="module")
 def group(dev):
-    if not dist.is_initialized():
+    owned = not dist.is_initialized()
+    if owned:
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                                 device_id=dev)
     yield
-    # the group stays for the session (RCCL teardown mid-session is not needed)
+    if owned:
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
 
 
 class _Net(nn.Module):
