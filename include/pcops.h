@@ -207,6 +207,16 @@ int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int 
                         const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
                         void *dx16, float *dgamma, float *dbeta, void *workspace, unsigned long long workspace_bytes,
                         pcops_stream_t stream);
+/* pcops_layernorm_bwd_colsum: pcops_layernorm_bwd plus dsum[c] = sum_r dx[r][c] (C fp32):
+ *   the bias gradient of the Linear / 1x1 conv whose output is a LayerNorm input (a or b),
+ *   summed over dx as stored -- dx16's bf16 values (dsum_src = 1) or dx32's (dsum_src = 0) --
+ *   in the same launch (replaces that layer's separate pcops_colsum over dx).
+ *   workspace: pcops_layernorm_bwd_colsum_workspace_bytes. */
+unsigned long long pcops_layernorm_bwd_colsum_workspace_bytes(int rows, int C);
+int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b,
+                               int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
+                               float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
+                               void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_colsum: out[c] = sum_r g[r][c] over a row-major (rows, C) matrix, C % 8 == 0,
  *   fp32 accumulation in a fixed order (deterministic); g / out dtype codes 0 fp32, 1 bf16.
  *   Replaces the bias-gradient reduction autograd runs for nn.Linear / 1x1 nn.Conv*d biases

@@ -121,7 +121,7 @@ class _TransposeAdd:
 
 class _LayerNorm:
     @staticmethod
-    def apply(a, b, weight, bias, eps, want16):
+    def apply(a, b, weight, bias, eps, want16, sum_of=None):  # sum_of: a GPU-only fusion
         x = (a if b is None else a + b).float()
         y = torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps)
         return (y, y.to(torch.bfloat16)) if want16 else y

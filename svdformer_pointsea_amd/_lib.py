@@ -55,6 +55,8 @@ _SIGS = {
     "pcops_layernorm_fwd": (I, [P, I, P, I, P, P, F, I, I, P, P, P, P, P]),
     "pcops_layernorm_bwd_workspace_bytes": (ULL, [I, I]),
     "pcops_layernorm_bwd": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, ULL, P]),
+    "pcops_layernorm_bwd_colsum_workspace_bytes": (ULL, [I, I]),
+    "pcops_layernorm_bwd_colsum": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, I, P, ULL, P]),
     "pcops_colsum_workspace_bytes": (ULL, [LL, I]),
     "pcops_colsum": (I, [P, I, LL, I, P, I, P, ULL, P]),
     "pcops_pcsa_forward": (I, [P, I, P, I, P, I, I, I, P, P]),

@@ -95,8 +95,14 @@ class _Linear(Function):
             if ctx.needs_input_grad[1]:
                 gw = _wgrad(g2.contiguous(), x.reshape(-1, x.shape[-1]).contiguous(), w.dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = colsum(g2.contiguous())
+            # a LayerNorm backward that consumed this output may have summed g
+            # already (pcops_layernorm_bwd_colsum, attached to g); else one colsum
+            pre = getattr(g, _PRESUM, None)
+            gb = pre if pre is not None else colsum(g2.contiguous())
         return gx, gw, gb
+
+
+_PRESUM = "_pcops_bias_colsum"   # attribute a gradient tensor carries when its column sum is known
 
 
 class _nullctx:
@@ -334,10 +340,15 @@ def _want_bf16():
 
 
 class _LayerNorm(Function):
-    """y = LayerNorm(a (+ b)) over the last dim -> (y fp32, y bf16 or None)."""
+    """y = LayerNorm(a (+ b)) over the last dim -> (y fp32, y bf16 or None).
+
+    sum_of (0 = a, 1 = b, None): that input is the output of a biased Linear
+    (the _Linear path); the backward then also column-sums its gradient in the
+    same launch and attaches the sum to the gradient it returns, which the
+    Linear's backward uses as its bias gradient instead of a separate colsum."""
 
     @staticmethod
-    def forward(ctx, a, b, weight, bias, eps, want16):
+    def forward(ctx, a, b, weight, bias, eps, want16, sum_of=None):
         _cuda_only("layer_norm", a, b)
         a = a.contiguous()
         b = None if b is None else b.contiguous()
@@ -353,6 +364,7 @@ class _LayerNorm(Function):
                  ptr(w), ptr(bb), float(eps), rows, C, ptr(y32), ptr(y16), ptr(mean), ptr(rstd), stream_of(a))
         ctx.save_for_backward(a, b, w, mean, rstd)
         ctx.wdt = weight.dtype
+        ctx.sum_of = sum_of
         if y16 is None:
             return y32
         return y32, y16
@@ -369,24 +381,54 @@ class _LayerNorm(Function):
         dx16 = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device) if torch.bfloat16 in dtypes else None
         dw = torch.empty(C, dtype=torch.float32, device=a.device)
         db = torch.empty_like(dw)
-        wsb = lib().pcops_layernorm_bwd_workspace_bytes(rows, C)
-        ws = _lib.Workspace.get(a.device, wsb)
-        with torch.cuda.device(a.device):
-            call("layernorm_bwd", lib().pcops_layernorm_bwd, ptr(g32), ptr(g16), ptr(a), _dt(a), ptr(b),
-                 0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16), ptr(dw),
-                 ptr(db), ptr(ws), wsb, stream_of(a))
+        src = None if ctx.sum_of is None else (a, b)[ctx.sum_of]
+        need = (ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        if src is not None and need[ctx.sum_of]:
+            dsum = torch.empty_like(dw)
+            wsb = lib().pcops_layernorm_bwd_colsum_workspace_bytes(rows, C)
+            ws = _lib.Workspace.get(a.device, wsb)
+            with torch.cuda.device(a.device):
+                call("layernorm_bwd", lib().pcops_layernorm_bwd_colsum, ptr(g32), ptr(g16), ptr(a), _dt(a), ptr(b),
+                     0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16),
+                     ptr(dw), ptr(db), ptr(dsum), _DT[src.dtype], ptr(ws), wsb, stream_of(a))
+        else:
+            dsum = None
+            wsb = lib().pcops_layernorm_bwd_workspace_bytes(rows, C)
+            ws = _lib.Workspace.get(a.device, wsb)
+            with torch.cuda.device(a.device):
+                call("layernorm_bwd", lib().pcops_layernorm_bwd, ptr(g32), ptr(g16), ptr(a), _dt(a), ptr(b),
+                     0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16),
+                     ptr(dw), ptr(db), ptr(ws), wsb, stream_of(a))
         pick = {torch.float32: dx32, torch.bfloat16: dx16}
         ga = pick[a.dtype]
         gb = None if b is None else pick[b.dtype]
-        return ga, gb, dw.to(ctx.wdt), db.to(ctx.wdt), None, None
+        if dsum is not None:
+            # a and b may share one gradient tensor: the sum goes on a view
+            # of its own, so only the summed input's producer sees it
+            g = ga.view_as(ga) if ctx.sum_of == 0 else gb.view_as(gb)
+            setattr(g, _PRESUM, dsum)
+            if ctx.sum_of == 0:
+                ga = g
+            else:
+                gb = g
+        return ga, gb, dw.to(ctx.wdt), db.to(ctx.wdt), None, None, None
 
 
-def layer_norm(norm, a, b=None):
-    """norm(a (+ b)) -> (fp32 output, GEMM operand: its bf16 copy under autocast)."""
+def layer_norm(norm, a, b=None, sum_of=None):
+    """norm(a (+ b)) -> (fp32 output, GEMM operand: its bf16 copy under autocast).
+    sum_of: see _LayerNorm (only taken when that input came from _Linear)."""
+    if sum_of is not None and not _from_linear((a, b)[sum_of]):
+        sum_of = None
     if _want_bf16():
-        return _LayerNorm.apply(a, b, norm.weight, norm.bias, norm.eps, True)
-    y = _LayerNorm.apply(a, b, norm.weight, norm.bias, norm.eps, False)
+        return _LayerNorm.apply(a, b, norm.weight, norm.bias, norm.eps, True, sum_of)
+    y = _LayerNorm.apply(a, b, norm.weight, norm.bias, norm.eps, False, sum_of)
     return y, y
+
+
+def _from_linear(t):
+    """t is the output of a biased _Linear whose bias needs a gradient."""
+    fn = t.grad_fn if t is not None else None
+    return fn is not None and type(fn).__name__ == "_LinearBackward" and _FUSED_BIAS_SUM
 
 
 def _conv1x1_tokens(conv, x_tok):
@@ -419,14 +461,14 @@ class _BlockBase(nn.Module):
 
     def _tail(self, s1, attn):
         """norm12(s1 + attn) -> FFN -> (residual stream fp32, FFN output)."""
-        s2, s2h = layer_norm(self.norm12, s1, attn)
+        s2, s2h = layer_norm(self.norm12, s1, attn, sum_of=1)   # attn = out_proj(...)
         h = self.activation1(linear(s2h, self.linear11.weight, self.linear11.bias))
         f = linear(h, self.linear12.weight, self.linear12.bias)
         return s2, f
 
     def _in(self, x_tok):
         y = _conv1x1_tokens(self.input_proj, x_tok) if hasattr(self, "input_proj") else x_tok
-        return layer_norm(self.norm13, y)
+        return layer_norm(self.norm13, y, sum_of=0 if hasattr(self, "input_proj") else None)
 
 
 class _AddToBf16(Function):
@@ -457,6 +499,7 @@ def block_sum(s, f):
 
 
 _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
+_FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
 
 
 def _pos_tokens(pos):

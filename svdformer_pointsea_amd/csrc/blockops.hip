@@ -176,22 +176,29 @@ int ln_bwd_rpw(int rows) {
 }
 
 // CH: 8-element chunks per lane (1 for C <= 512, 2 for C <= 1024); AT / BT as
-// the forward; GM: which upstream gradients are present (1 = dy32, 2 = dy16, 3 both)
-template <int CH, int AT, int BT, int GM>
+// the forward; GM: which upstream gradients are present (1 = dy32, 2 = dy16,
+// 3 both); CS: also the column sums of dx (the bias gradient of the Linear
+// whose output is a or b) over the values as stored -- bf16-rounded when
+// sum16 -- as a third C-wide partial row.
+template <int CH, int AT, int BT, int GM, bool CS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4 : 3))) void ln_bwd_kernel(
     const float *__restrict__ g32, const __bf16 *__restrict__ g16, const void *__restrict__ a,
     const void *__restrict__ b, const float *__restrict__ gamma, const float *__restrict__ mean_in,
     const float *__restrict__ rstd_in, int rows, int C, float *__restrict__ dx32, __bf16 *__restrict__ dx16, int rpw,
-    float *__restrict__ part) {
-  extern __shared__ float ln_red[];  // [4][2C]
+    float *__restrict__ part, bool sum16) {
+  constexpr int NP = CS ? 3 : 2;     // partial rows per block: dgamma | dbeta (| dsum)
+  extern __shared__ float ln_red[];  // [4][NP*C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = C >> 3;
-  V8 dg[CH], db[CH], gm[CH];
+  V8 dg[CH], db[CH], gm[CH], dsm[CS ? CH : 1];
 #pragma unroll
   for (int i = 0; i < CH; ++i) {
     ld8c<0>(gm[i], gamma, 8 * min(lane + 64 * i, nch - 1));  // hoisted out of the row loop
 #pragma unroll
     for (int k = 0; k < 8; ++k) dg[i].v[k] = db[i].v[k] = 0.f;
+    if constexpr (CS)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dsm[i].v[k] = 0.f;
   }
   const int r0 = (blockIdx.x * 4 + w) * rpw;
   for (int row = r0; row < r0 + rpw && row < rows; ++row) {
@@ -243,6 +250,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
         for (int k = 0; k < 8; ++k) dx.v[k] = rstd * (dy[i].v[k] * gm[i].v[k] - mg - xh[i].v[k] * mgx);
         if (dx32) st8_f32(dx32, base + 8 * ch, dx);
         if (dx16) st8_bf16(dx16, base + 8 * ch, dx);
+        if constexpr (CS)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dsm[i].v[k] += sum16 ? (float)(__bf16)dx.v[k] : dx.v[k];
       }
     }
   }
@@ -252,14 +262,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
     if (ch < nch)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        ln_red[w * 2 * C + 8 * ch + k] = dg[i].v[k];
-        ln_red[w * 2 * C + C + 8 * ch + k] = db[i].v[k];
+        ln_red[w * NP * C + 8 * ch + k] = dg[i].v[k];
+        ln_red[w * NP * C + C + 8 * ch + k] = db[i].v[k];
+        if constexpr (CS) ln_red[w * NP * C + 2 * C + 8 * ch + k] = dsm[i].v[k];
       }
   }
   __syncthreads();
-  float *pb = part + (long long)blockIdx.x * 2 * C;
-  for (int c = threadIdx.x; c < 2 * C; c += 256)
-    pb[c] = ((ln_red[c] + ln_red[2 * C + c]) + ln_red[4 * C + c]) + ln_red[6 * C + c];
+  float *pb = part + (long long)blockIdx.x * NP * C;
+  for (int c = threadIdx.x; c < NP * C; c += 256)
+    pb[c] = ((ln_red[c] + ln_red[NP * C + c]) + ln_red[2 * NP * C + c]) + ln_red[3 * NP * C + c];
 }
 
 // ---- host dispatch over the operand configurations
@@ -273,6 +284,7 @@ struct LnArgs {
   float *y32;
   __bf16 *y16;
   float *part;
+  bool cs, sum16;  // backward: fused bias column sum, over bf16-rounded dx
   hipStream_t s;
 };
 
@@ -285,8 +297,14 @@ void ln_fwd_go(const LnArgs &p) {
 
 template <int CH, int AT, int BT, int GM>
 void ln_bwd_go(const LnArgs &p, int blocks, int rpw) {
-  hipLaunchKernelGGL((ln_bwd_kernel<CH, AT, BT, GM>), dim3(blocks), dim3(256), 4 * 2 * p.C * sizeof(float), p.s,
-                     p.g32, p.g16, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16, rpw, p.part);
+  if (p.cs)
+    hipLaunchKernelGGL((ln_bwd_kernel<CH, AT, BT, GM, true>), dim3(blocks), dim3(256), 4 * 3 * p.C * sizeof(float),
+                       p.s, p.g32, p.g16, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16, rpw, p.part,
+                       p.sum16);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<CH, AT, BT, GM, false>), dim3(blocks), dim3(256), 4 * 2 * p.C * sizeof(float),
+                       p.s, p.g32, p.g16, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16, rpw, p.part,
+                       false);
 }
 
 // CH x AT x BT resolved at compile time from runtime codes (bt = -1: no b)
@@ -384,10 +402,12 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restr
   }
 }
 
-// columns [0, split) go to out, [split, C) to out2 (the LayerNorm's dgamma | dbeta)
+// columns [0, split) go to out, [split, split2) to out2, [split2, C) to out3
+// (the LayerNorm's dgamma | dbeta | fused bias sum, all in odt)
 __global__ __launch_bounds__(1024) void colsum_final_kernel(const float *__restrict__ part, int chunks, int C,
                                                             void *__restrict__ out, int odt, int split,
-                                                            void *__restrict__ out2) {
+                                                            void *__restrict__ out2, int split2,
+                                                            void *__restrict__ out3) {
   __shared__ float red[32][33];
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + cl;
@@ -403,8 +423,10 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float *__restr
     for (int i = 0; i < 32; ++i) tot += red[i][cl];
     if (col < split)
       st(out, odt, col, tot);
-    else
+    else if (col < split2)
       st(out2, odt, col - split, tot);
+    else
+      st(out3, odt, col - split2, tot);
   }
 }
 
@@ -480,24 +502,27 @@ extern "C" unsigned long long pcops_layernorm_bwd_workspace_bytes(int rows, int 
   return (unsigned long long)ln_bwd_blocks(rows) * 2 * C * sizeof(float);
 }
 
-extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b,
-                                   int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows,
-                                   int C, float *dx32, void *dx16, float *dgamma, float *dbeta, void *workspace,
-                                   unsigned long long workspace_bytes, pcops_stream_t stream) {
+namespace {
+int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b, int b_dtype,
+                       const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
+                       void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src, void *workspace,
+                       unsigned long long workspace_bytes, unsigned long long need, hipStream_t s) {
   if (rows < 0 || C <= 0) return PCOPS_ERR_INVALID;
   if (C > 512 * kMaxCh || C % 8) return PCOPS_ERR_UNSUPPORTED;
   if (!dgamma || !dbeta) return PCOPS_ERR_INVALID;
-  hipStream_t s = (hipStream_t)stream;
+  if (dsum && ((dsum_src == 1 && !dx16) || (dsum_src == 0 && !dx32) || (dsum_src != 0 && dsum_src != 1)))
+    return PCOPS_ERR_INVALID;
   if (rows == 0) {
     if (hipMemsetAsync(dgamma, 0, sizeof(float) * C, s) != hipSuccess ||
-        hipMemsetAsync(dbeta, 0, sizeof(float) * C, s) != hipSuccess)
+        hipMemsetAsync(dbeta, 0, sizeof(float) * C, s) != hipSuccess ||
+        (dsum && hipMemsetAsync(dsum, 0, sizeof(float) * C, s) != hipSuccess))
       return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!a || !gamma || !mean || !rstd || (!dy32 && !dy16) || (!dx32 && !dx16) || !dt_ok(a_dtype) ||
       (b && !dt_ok(b_dtype)))
     return PCOPS_ERR_INVALID;
-  if (!workspace || workspace_bytes < pcops_layernorm_bwd_workspace_bytes(rows, C)) return PCOPS_ERR_WORKSPACE;
+  if (!workspace || workspace_bytes < need) return PCOPS_ERR_WORKSPACE;
   const int blocks = ln_bwd_blocks(rows);
   float *part = (float *)workspace;
   LnArgs p{};
@@ -513,13 +538,42 @@ extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const vo
   p.y32 = dx32;
   p.y16 = (__bf16 *)dx16;
   p.part = part;
+  p.cs = dsum != nullptr;
+  p.sum16 = dsum_src == 1;
   p.s = s;
   ln_dispatch<LnBwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p, (dy32 ? 1 : 0) | (dy16 ? 2 : 0), blocks,
                       ln_bwd_rpw(rows));
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((2 * C + 31) / 32), dim3(1024), 0, s, part, blocks, 2 * C,
-                     (void *)dgamma, 0, C, (void *)dbeta);
+  const int np = dsum ? 3 : 2;
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((np * C + 31) / 32), dim3(1024), 0, s, part, blocks, np * C,
+                     (void *)dgamma, 0, C, (void *)dbeta, 2 * C, (void *)dsum);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
+}
+}  // namespace
+
+extern "C" int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b,
+                                   int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows,
+                                   int C, float *dx32, void *dx16, float *dgamma, float *dbeta, void *workspace,
+                                   unsigned long long workspace_bytes, pcops_stream_t stream) {
+  return layernorm_bwd_impl(dy32, dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, dx16, dgamma, dbeta,
+                            nullptr, 0, workspace, workspace_bytes, pcops_layernorm_bwd_workspace_bytes(rows, C),
+                            (hipStream_t)stream);
+}
+
+extern "C" unsigned long long pcops_layernorm_bwd_colsum_workspace_bytes(int rows, int C) {
+  if (rows <= 0 || C <= 0) return 0;
+  return (unsigned long long)ln_bwd_blocks(rows) * 3 * C * sizeof(float);
+}
+
+extern "C" int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *a, int a_dtype,
+                                          const void *b, int b_dtype, const float *gamma, const float *mean,
+                                          const float *rstd, int rows, int C, float *dx32, void *dx16, float *dgamma,
+                                          float *dbeta, float *dsum, int dsum_src, void *workspace,
+                                          unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (!dsum) return PCOPS_ERR_INVALID;
+  return layernorm_bwd_impl(dy32, dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, dx16, dgamma, dbeta,
+                            dsum, dsum_src, workspace, workspace_bytes,
+                            pcops_layernorm_bwd_colsum_workspace_bytes(rows, C), (hipStream_t)stream);
 }
 
 extern "C" unsigned long long pcops_colsum_workspace_bytes(long long rows, int C) {
@@ -552,7 +606,7 @@ extern "C" int pcops_colsum(const void *g, int g_dtype, long long rows, int C, v
   else
     hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, out, out_dtype, C,
-                     nullptr);
+                     nullptr, C, nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

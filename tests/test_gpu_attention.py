@@ -589,3 +589,38 @@ def _block_module(c, dev):
     else:
         m = A.SDG_Decoder(c["cin"], c["cout"], c["ratio"])
     return fill_state(m, seed=c["wseed"]).eval().to(dev)
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
+    """input_proj / out_proj bias gradients summed inside the LayerNorm backward
+    (pcops_layernorm_bwd_colsum) equal the separate colsum path; the separate
+    colsum runs for exactly those two layers fewer."""
+    import copy
+
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(0)
+    blk = A.self_attention(64, 128, nhead=2).to(dev)
+    x = torch.randn(4, 64, 2048, device=dev)            # 8192 tokens: the _Linear path
+    calls = []
+    real = A.colsum
+    monkeypatch.setattr(A, "colsum", lambda g: calls.append(g.shape) or real(g))
+
+    def run(fused):
+        monkeypatch.setattr(A, "_FUSED_BIAS_SUM", fused)
+        m = copy.deepcopy(blk)
+        calls.clear()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = m(x)
+        (y.float() ** 2).mean().backward()
+        return {n: p.grad.float().clone() for n, p in m.named_parameters()}, len(calls)
+
+    g_ref, n_ref = run(False)
+    g_fus, n_fus = run(True)
+    assert n_ref - n_fus == 2, (n_ref, n_fus)
+    for n in g_ref:
+        # fused sums are fp32 over the stored (bf16 under autocast) dx; the
+        # separate colsum rounds its result to the gradient's dtype
+        tol = dict(rtol=1e-2, atol=1e-5) if amp else dict(rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(g_fus[n], g_ref[n], **tol, msg=n)
