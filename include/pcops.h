@@ -192,6 +192,11 @@ int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const v
  *   out2 (optional) receives the same values in out2_dtype. */
 int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype, void *out2,
                         int out2_dtype, int B, int R, int C, pcops_stream_t stream);
+/* pcops_add: out[i] = a[i] + b[i] for i < n in the promoted dtype (fp32 unless both are bf16),
+ * stored as out_dtype (torch.add(a, b, out=out) with type promotion; the attention blocks' residual + FFN sum
+ * that feeds only GEMMs, models/model_utils.py:616).  16-byte aligned operands. */
+int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype, long long n,
+              pcops_stream_t stream);
 /* pcops_layernorm_fwd: x = a (+ b); y = (x - mean) * rstd * gamma + beta per row
  * (torch.nn.LayerNorm over the last dim), written as fp32 (y32) and/or bf16
  * (y16); mean / rstd (rows) saved for the backward.  C <= 1024, C % 8 == 0,

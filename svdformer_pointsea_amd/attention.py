@@ -480,7 +480,12 @@ class _AddToBf16(Function):
     @staticmethod
     def forward(ctx, a, b):
         out = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
-        torch.add(a, b, out=out)
+        if _PCOPS_ADD and a.shape == b.shape and a.dtype in _DT and b.dtype in _DT:
+            a, b = a.contiguous(), b.contiguous()
+            with torch.cuda.device(a.device):
+                call("add", lib().pcops_add, ptr(a), _dt(a), ptr(b), _dt(b), ptr(out), 1, a.numel(), stream_of(a))
+        else:   # broadcasting (never in the models): torch's add
+            torch.add(a, b, out=out)
         ctx.dts = (a.dtype, b.dtype)
         return out
 
@@ -500,6 +505,7 @@ def block_sum(s, f):
 
 _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
 _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
+_PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
 
 
 def _pos_tokens(pos):

@@ -356,6 +356,47 @@ int ln_bwd_blocks(int rows) {
 
 bool dt_ok(int dt) { return dt == 0 || dt == 1; }
 
+// ---------------------------------------------------------------- add
+// out = a + b in the promoted dtype (fp32 unless both are bf16), then the
+// output dtype: torch.add(a, b, out=out) with type promotion (fp32 + bf16 -> bf16 is the block outputs that
+// feed only GEMMs).  torch runs mixed-dtype adds on its unvectorised dynamic-
+// cast kernel (~2.5x the HBM time); here 8 elements per thread, 16-B accesses.
+template <int AT, int BT, int OT>
+__global__ __launch_bounds__(256) void add_kernel(const void *__restrict__ a, const void *__restrict__ b,
+                                                  void *__restrict__ out, long long n8) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    V8 x, y;
+    ld8c<AT>(x, a, 8 * i);
+    ld8c<BT>(y, b, 8 * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      x.v[k] += y.v[k];
+      if constexpr (AT == 1 && BT == 1) x.v[k] = (float)(__bf16)x.v[k];  // promoted dtype bf16
+    }
+    if constexpr (OT == 0)
+      st8_f32(reinterpret_cast<float *>(out), 8 * i, x);
+    else
+      st8_bf16(reinterpret_cast<__bf16 *>(out), 8 * i, x);
+  }
+}
+
+__global__ void add_tail_kernel(const void *__restrict__ a, int adt, const void *__restrict__ b, int bdt,
+                                void *__restrict__ out, int odt, long long i0, long long n) {
+  const long long i = i0 + threadIdx.x;
+  if (i < n) {
+    float v = ld(a, adt, i) + ld(b, bdt, i);
+    if (adt == 1 && bdt == 1) v = (float)(__bf16)v;  // promoted dtype bf16
+    st(out, odt, i, v);
+  }
+}
+
+template <int AT, int BT, int OT>
+void add_go(const void *a, const void *b, void *out, long long n8, hipStream_t s) {
+  long long g = (n8 + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL((add_kernel<AT, BT, OT>), dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, s, a, b, out, n8);
+}
+
 // ---------------------------------------------------------------- column sum
 // out[c] = sum_r g[r][c]: the bias gradient of the blocks' Linear / 1x1-conv
 // layers (torch's bf16 sum(0) runs at 0.8-3 TB/s on these (65536, C) inputs).
@@ -457,6 +498,34 @@ void colsum_shape(long long rows, int C, int &chunks, long long &rpc) {
 }
 
 }  // namespace
+
+extern "C" int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype,
+                         long long n, pcops_stream_t stream) {
+  if (n < 0 || !dt_ok(a_dtype) || !dt_ok(b_dtype) || !dt_ok(out_dtype)) return PCOPS_ERR_INVALID;
+  if (n == 0) return PCOPS_OK;
+  if (!a || !b || !out) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  const long long n8 = n / 8;
+  if (n8 > 0) {
+    const int code = a_dtype * 4 + b_dtype * 2 + out_dtype;
+    switch (code) {
+      case 0: add_go<0, 0, 0>(a, b, out, n8, s); break;
+      case 1: add_go<0, 0, 1>(a, b, out, n8, s); break;
+      case 2: add_go<0, 1, 0>(a, b, out, n8, s); break;
+      case 3: add_go<0, 1, 1>(a, b, out, n8, s); break;
+      case 4: add_go<1, 0, 0>(a, b, out, n8, s); break;
+      case 5: add_go<1, 0, 1>(a, b, out, n8, s); break;
+      case 6: add_go<1, 1, 0>(a, b, out, n8, s); break;
+      default: add_go<1, 1, 1>(a, b, out, n8, s); break;
+    }
+    PC_CHECK_LAUNCH();
+  }
+  if (n8 * 8 < n) {
+    hipLaunchKernelGGL(add_tail_kernel, dim3(1), dim3(64), 0, s, a, a_dtype, b, b_dtype, out, out_dtype, n8 * 8, n);
+    PC_CHECK_LAUNCH();
+  }
+  return PCOPS_OK;
+}
 
 extern "C" int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype,
                                    void *out2, int out2_dtype, int B, int R, int C, pcops_stream_t stream) {

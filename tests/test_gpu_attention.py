@@ -624,3 +624,32 @@ def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
         # separate colsum rounds its result to the gradient's dtype
         tol = dict(rtol=1e-2, atol=1e-5) if amp else dict(rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(g_fus[n], g_ref[n], **tol, msg=n)
+
+
+@pytest.mark.parametrize("n", [8, 1000, 1003, 1 << 20])
+def test_add_kernel_bitwise(dev, n):
+    """pcops_add: the sum in the promoted dtype (fp32 unless both operands are
+    bf16), stored as the output dtype -- bitwise, every dtype combination,
+    including a non-multiple-of-8 tail.  torch.add(out=bf16) agrees for the
+    combination the blocks use (fp32 residual + bf16 FFN output); for a bf16
+    FIRST operand with an fp32 second it rounds the fp32 operand to bf16 before
+    adding (measured), which is not the promoted-dtype sum."""
+    from svdformer_pointsea_amd._lib import call, lib, ptr, stream_of
+    from svdformer_pointsea_amd.attention import _DT
+
+    g = torch.Generator().manual_seed(n)
+    for adt in (torch.float32, torch.bfloat16):
+        for bdt in (torch.float32, torch.bfloat16):
+            for odt in (torch.float32, torch.bfloat16):
+                a = (torch.randn(n, generator=g) * 3).to(adt).to(dev)
+                b = (torch.randn(n, generator=g) * 3).to(bdt).to(dev)
+                out = torch.empty(n, dtype=odt, device=dev)
+                call("add", lib().pcops_add, ptr(a), _DT[adt], ptr(b), _DT[bdt], ptr(out), _DT[odt], n,
+                     stream_of(a))
+                both16 = adt == bdt == torch.bfloat16
+                ref = (a.float() + b.float()).to(torch.bfloat16 if both16 else torch.float32).to(odt)
+                assert torch.equal(out, ref), (adt, bdt, odt)
+                if (adt, bdt, odt) == (torch.float32, torch.bfloat16, torch.bfloat16):
+                    tref = torch.empty(n, dtype=odt, device=dev)
+                    torch.add(a, b, out=tref)
+                    assert torch.equal(out, tref)

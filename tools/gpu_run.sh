@@ -77,6 +77,13 @@ run_stage() {
         env $g timeout -k 10 120 python tools/attn_bench.py ${ATTN_SHAPES:-0 1 2 3} >> "$OUT/attn_ab.txt" 2>&1 || return 1
       done ;;
     step_profile) timeout -k 10 400 python tools/step_profile.py --rows 60 > "$OUT/step_ops.txt" 2>&1 ;;
+    bench_ab)  # quick same-box A/B of the PCN step: one short bench per env group in $BENCH_AB ("A=1;A=0")
+      IFS=';' read -ra groups <<< "${BENCH_AB:?set BENCH_AB}"
+      for g in "${groups[@]}"; do
+        echo "== $g" >> "$OUT/bench_ab.txt"
+        env $g timeout -k 10 400 python bench.py --no-cpu-baseline --no-fp32-leg --no-kernel-timing --steps 20 \
+          --warmup 3 >> "$OUT/bench_ab.txt" 2>> "$OUT/bench_ab.err" || return 1
+      done ;;
     avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
     knn) timeout -k 10 120 python tools/knn_bench.py > "$OUT/knn_bench.txt" 2>&1 ;;
     chamfer) timeout -k 10 120 python tools/microbench.py > "$OUT/chamfer_bench.txt" 2>&1 ;;
