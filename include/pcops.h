@@ -222,6 +222,13 @@ int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *
                                int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
                                float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
                                void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+/* pcops_gelu_bwd_colsum: du = dy * GELU'(u) (exact erf GELU, torch's GeluBackward expression in
+ *   fp32) over a row-major (rows, C) matrix, dy / u / du all `dtype` (0 fp32, 1 bf16), C % 8 == 0;
+ *   when dsum != NULL also dsum[c] = sum_r du[r][c] over du as stored (C fp32): the bias gradient
+ *   of the Linear whose output u the GELU consumed (the blocks' linear11, models/model_utils.py:612),
+ *   in place of a separate pcops_colsum.  workspace: pcops_colsum_workspace_bytes(rows, C) when dsum. */
+int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, long long rows, int C, void *du, float *dsum,
+                          void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_colsum: out[c] = sum_r g[r][c] over a row-major (rows, C) matrix, C % 8 == 0,
  *   fp32 accumulation in a fixed order (deterministic); g / out dtype codes 0 fp32, 1 bf16.
  *   Replaces the bias-gradient reduction autograd runs for nn.Linear / 1x1 nn.Conv*d biases

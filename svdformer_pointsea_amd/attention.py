@@ -426,9 +426,51 @@ def layer_norm(norm, a, b=None, sum_of=None):
 
 
 def _from_linear(t):
-    """t is the output of a biased _Linear whose bias needs a gradient."""
+    """t is the output of a biased _Linear whose bias needs a gradient, issued
+    on the main stream.  Inside side-stream blocks the separate colsum stays:
+    there the pre-summed tensor crossed streams between its producer and the
+    Linear's backward and the captured step produced non-finite losses
+    (measured; the fused sums are a main-stream optimisation only)."""
     fn = t.grad_fn if t is not None else None
-    return fn is not None and type(fn).__name__ == "_LinearBackward" and _FUSED_BIAS_SUM
+    return (fn is not None and type(fn).__name__ == "_LinearBackward" and _FUSED_BIAS_SUM
+            and not _lib.on_side_stream())
+
+
+class _Gelu(Function):
+    """Exact (erf) GELU whose backward is pcops_gelu_bwd_colsum: with the input
+    the output of a biased _Linear, the same launch column-sums du and hands
+    the sum to that Linear's backward (its bias gradient), like _LayerNorm."""
+
+    @staticmethod
+    def forward(ctx, u, want_sum):
+        ctx.save_for_backward(u)
+        ctx.want_sum = want_sum
+        return F.gelu(u)
+
+    @staticmethod
+    def backward(ctx, g):
+        (u,) = ctx.saved_tensors
+        g = g.contiguous().to(u.dtype)
+        C = u.shape[-1]
+        rows = u.numel() // C
+        du = torch.empty_like(u)
+        dsum = torch.empty(C, dtype=torch.float32, device=u.device) if ctx.want_sum else None
+        wsb = lib().pcops_colsum_workspace_bytes(rows, C) if ctx.want_sum else 0
+        ws = _lib.Workspace.get(u.device, wsb) if ctx.want_sum else None
+        with torch.cuda.device(u.device):
+            call("gelu_bwd", lib().pcops_gelu_bwd_colsum, ptr(g), ptr(u), _dt(u), rows, C, ptr(du), ptr(dsum),
+                 ptr(ws), wsb, stream_of(u))
+        if dsum is not None:
+            setattr(du, _PRESUM, dsum)
+        return du, None
+
+
+def gelu(act, u):
+    """act(u) for the blocks' nn.GELU(): the fused-backward _Gelu on CUDA."""
+    if (_PCOPS_GELU and u.is_cuda and isinstance(act, nn.GELU) and act.approximate == "none" and u.dtype in _DT
+            and u.shape[-1] % 8 == 0 and u.is_contiguous() and torch.is_grad_enabled() and u.requires_grad):
+        return _Gelu.apply(u, _from_linear(u))
+    return act(u)
 
 
 def _conv1x1_tokens(conv, x_tok):
@@ -462,7 +504,7 @@ class _BlockBase(nn.Module):
     def _tail(self, s1, attn):
         """norm12(s1 + attn) -> FFN -> (residual stream fp32, FFN output)."""
         s2, s2h = layer_norm(self.norm12, s1, attn, sum_of=1)   # attn = out_proj(...)
-        h = self.activation1(linear(s2h, self.linear11.weight, self.linear11.bias))
+        h = gelu(self.activation1, linear(s2h, self.linear11.weight, self.linear11.bias))
         f = linear(h, self.linear12.weight, self.linear12.bias)
         return s2, f
 
@@ -506,6 +548,7 @@ def block_sum(s, f):
 _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
 _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
 _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
+_PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
 
 
 def _pos_tokens(pos):

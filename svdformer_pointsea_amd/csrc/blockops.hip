@@ -471,6 +471,64 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float *__restr
   }
 }
 
+// GELU backward (exact erf form, torch's GeluBackward expression in fp32) fused
+// with the column sum of its output -- the bias gradient of the Linear whose
+// output the GELU consumed -- in colsum_partial_kernel's launch shape:
+//   du = dy * (Phi(u) + u * phi(u)),  partial[chunk][c] = sum over the chunk's rows of du as stored.
+// SUM = false: the GELU backward alone.
+template <int DT, bool SUM>
+__global__ __launch_bounds__(256) void gelu_bwd_partial_kernel(const void *__restrict__ dy, const void *__restrict__ u,
+                                                               void *__restrict__ du, long long rows, int C, int V,
+                                                               long long rpc, float *__restrict__ part) {
+  __shared__ float red[4][64 * 8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rw = 64 / V;
+  const int rsub = lane / V, vi = lane - rsub * V;
+  const int col = (blockIdx.y * V + vi) * 8;
+  const long long r0 = blockIdx.x * rpc, r1 = min(rows, r0 + rpc);
+  constexpr float kAlpha = 0.70710678118654752440f;                      // M_SQRT1_2
+  constexpr float kBeta = 1.12837916709551257390f * 0.70710678118654752440f * 0.5f;  // M_2_SQRTPI * M_SQRT1_2 / 2
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const long long step = 4LL * rw;
+#pragma unroll 4
+  for (long long r = r0 + w * rw + rsub; r < r1; r += step) {
+    V8 g, x, o;
+    ld8c<DT>(g, dy, r * C + col);
+    ld8c<DT>(x, u, r * C + col);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float cdf = 0.5f * (1.0f + erff(x.v[k] * kAlpha));
+      const float pdf = expf(-0.5f * x.v[k] * x.v[k]) * kBeta;
+      o.v[k] = g.v[k] * (cdf + x.v[k] * pdf);
+    }
+    if constexpr (DT == 0) {
+      st8_f32(reinterpret_cast<float *>(du), r * C + col, o);
+    } else {
+      st8_bf16(reinterpret_cast<__bf16 *>(du), r * C + col, o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o.v[k] = (float)(__bf16)o.v[k];  // the sum sees du as stored
+    }
+    if constexpr (SUM)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += o.v[k];
+  }
+  if constexpr (SUM) {
+    for (int o = V; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+    if (rsub == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[w][vi * 8 + k] = acc[k];
+    __syncthreads();
+    for (int i = threadIdx.x; i < V * 8; i += 256) {
+      const float sm = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+      part[blockIdx.x * (long long)C + blockIdx.y * V * 8 + i] = sm;
+    }
+  }
+}
+
 int colsum_v(int C) {  // vector columns per wave: largest power of two <= 64 dividing C / 8
   const int nv = C / 8;
   int V = 64;
@@ -651,6 +709,43 @@ extern "C" unsigned long long pcops_colsum_workspace_bytes(long long rows, int C
   long long rpc;
   colsum_shape(rows, C, chunks, rpc);
   return (unsigned long long)chunks * C * sizeof(float);
+}
+
+extern "C" int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, long long rows, int C, void *du,
+                                     float *dsum, void *workspace, unsigned long long workspace_bytes,
+                                     pcops_stream_t stream) {
+  if (rows < 0 || C <= 0 || !dt_ok(dtype)) return PCOPS_ERR_INVALID;
+  if (C % 8) return PCOPS_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  if (rows == 0) {
+    if (dsum && hipMemsetAsync(dsum, 0, sizeof(float) * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!dy || !u || !du) return PCOPS_ERR_INVALID;
+  if (dsum && (!workspace || workspace_bytes < pcops_colsum_workspace_bytes(rows, C))) return PCOPS_ERR_WORKSPACE;
+  int chunks;
+  long long rpc;
+  colsum_shape(rows, C, chunks, rpc);
+  const int V = colsum_v(C);
+  const dim3 grid(chunks, C / 8 / V);
+  float *part = (float *)workspace;
+  if (dsum) {
+    if (dtype == 0)
+      hipLaunchKernelGGL((gelu_bwd_partial_kernel<0, true>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc, part);
+    else
+      hipLaunchKernelGGL((gelu_bwd_partial_kernel<1, true>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc, part);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, (void *)dsum, 0,
+                       C, nullptr, C, nullptr);
+  } else {
+    if (dtype == 0)
+      hipLaunchKernelGGL((gelu_bwd_partial_kernel<0, false>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc,
+                         nullptr);
+    else
+      hipLaunchKernelGGL((gelu_bwd_partial_kernel<1, false>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc,
+                         nullptr);
+  }
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
 }
 
 extern "C" int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype,

@@ -594,8 +594,9 @@ def _block_module(c, dev):
 @pytest.mark.parametrize("amp", [False, True])
 def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
     """input_proj / out_proj bias gradients summed inside the LayerNorm backward
-    (pcops_layernorm_bwd_colsum) equal the separate colsum path; the separate
-    colsum runs for exactly those two layers fewer."""
+    (pcops_layernorm_bwd_colsum) and linear11's inside the GELU backward
+    (pcops_gelu_bwd_colsum) equal the separate colsum path; the separate
+    colsum runs for exactly those three layers fewer."""
     import copy
 
     from svdformer_pointsea_amd import attention as A
@@ -618,7 +619,7 @@ def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
 
     g_ref, n_ref = run(False)
     g_fus, n_fus = run(True)
-    assert n_ref - n_fus == 2, (n_ref, n_fus)
+    assert n_ref - n_fus == 3, (n_ref, n_fus)
     for n in g_ref:
         # fused sums are fp32 over the stored (bf16 under autocast) dx; the
         # separate colsum rounds its result to the gradient's dtype
@@ -653,3 +654,23 @@ def test_add_kernel_bitwise(dev, n):
                     tref = torch.empty(n, dtype=odt, device=dev)
                     torch.add(a, b, out=tref)
                     assert torch.equal(out, tref)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C", [(999, 1024), (8192, 3072), (300, 40)])
+def test_gelu_backward_kernel(dev, dt, rows, C):
+    """pcops_gelu_bwd_colsum vs torch's exact-GELU backward and g.sum(0)."""
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(rows)
+    u = (torch.randn(rows, C, device=dev) * 2).to(dt).requires_grad_(True)
+    g = torch.randn(rows, C, device=dev).to(dt)
+    h = A._Gelu.apply(u, True)
+    assert torch.equal(h, torch.nn.functional.gelu(u.detach()))
+    (du,) = torch.autograd.grad(h, u, g)
+    ur = u.detach().clone().requires_grad_(True)
+    (ref,) = torch.autograd.grad(torch.nn.functional.gelu(ur), ur, g)
+    tol = dict(rtol=1e-5, atol=1e-6) if dt == torch.float32 else dict(rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(du.float(), ref.float(), **tol)
+    dsum = getattr(du, A._PRESUM)
+    torch.testing.assert_close(dsum, du.float().sum(0), rtol=1e-4, atol=1e-3)
