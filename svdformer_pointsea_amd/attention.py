@@ -433,7 +433,7 @@ def _from_linear(t):
     (measured; the fused sums are a main-stream optimisation only)."""
     fn = t.grad_fn if t is not None else None
     return (fn is not None and type(fn).__name__ == "_LinearBackward" and _FUSED_BIAS_SUM
-            and not _lib.on_side_stream())
+            and (_FUSED_SIDE or not _lib.on_side_stream()))
 
 
 class _Gelu(Function):
@@ -469,7 +469,7 @@ def gelu(act, u):
     """act(u) for the blocks' nn.GELU(): the fused-backward _Gelu on CUDA."""
     if (_PCOPS_GELU and u.is_cuda and isinstance(act, nn.GELU) and act.approximate == "none" and u.dtype in _DT
             and u.shape[-1] % 8 == 0 and u.is_contiguous() and torch.is_grad_enabled() and u.requires_grad):
-        return _Gelu.apply(u, _from_linear(u))
+        return _Gelu.apply(u, _GELU_SUM and _from_linear(u))
     return act(u)
 
 
@@ -549,6 +549,12 @@ _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
 _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
 _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
 _PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
+_FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnostic: fused sums in side-stream blocks too
+# linear11's bias sum inside the GELU backward: off by default -- 2 of 4 bench
+# runs with it on ended with a non-finite loss in the timed steps, cause not
+# found (identical-input gradients match the separate colsum to bf16 noise,
+# and 50 graph replays without the optimizer stayed finite)
+_GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "0") == "1"
 
 
 def _pos_tokens(pos):

@@ -608,6 +608,8 @@ def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
     real = A.colsum
     monkeypatch.setattr(A, "colsum", lambda g: calls.append(g.shape) or real(g))
 
+    monkeypatch.setattr(A, "_GELU_SUM", True)
+
     def run(fused):
         monkeypatch.setattr(A, "_FUSED_BIAS_SUM", fused)
         m = copy.deepcopy(blk)
