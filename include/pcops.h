@@ -83,6 +83,16 @@ int pcops_sa_group(const float *xyz, const float *new_xyz, const float *points_t
 int pcops_sa_group_grad(const void *grad_out, int grad_dtype, const int *idx, int B, int N, int S, int K, int C,
                         float *grad_points_t, pcops_stream_t stream);
 
+/* pcops_max_k: torch.max(x, dim=3) of a (B, C, S, K) conv output held channels_last, i.e. over
+ *   the middle dim of a contiguous (rows = B*S, K, C) tensor (models/model_utils.py:354, 862-864):
+ *   out[r][c] = max_k x[r][k][c], arg[r][c] = the first maximising k (NaN is the maximum, as
+ *   torch).  dtype 0 fp32 / 1 bf16 for x and out; C % 8 == 0, K <= 255.
+ * pcops_max_k_grad: grad_x[r][k][c] = k == arg[r][c] ? grad_out[r][c] : 0 (fully written). */
+int pcops_max_k(const void *x, int dtype, long long rows, int K, int C, void *out, unsigned char *arg,
+                pcops_stream_t stream);
+int pcops_max_k_grad(const void *grad_out, int dtype, const unsigned char *arg, long long rows, int K, int C,
+                     void *grad_x, pcops_stream_t stream);
+
 /* ball_query(new_xyz, xyz, radius, nsample): ball_query.cpp:8-32, ball_query_gpu.cu:9-54.
  * new_xyz (B,M,3), xyz (B,N,3) -> idx (B,M,nsample). */
 int pcops_ball_query(const float *new_xyz, const float *xyz, int B, int N, int M, float radius, int nsample, int *idx,

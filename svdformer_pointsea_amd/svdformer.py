@@ -31,14 +31,55 @@ def _lin(conv, x):
     return linear(x, conv.weight.view(conv.weight.shape[0], -1), conv.bias)
 
 
+class _MaxK(torch.autograd.Function):
+    """max over K of a contiguous (B, S, K, C) tensor -> (B, S, C): pcops_max_k
+    (values and first-index argmax as torch.max) and pcops_max_k_grad (the
+    gradient written in one pass instead of zeros + scatter)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from ._lib import call, lib, ptr, stream_of
+
+        B, S, K, C = x.shape
+        out = torch.empty(B, S, C, dtype=x.dtype, device=x.device)
+        arg = torch.empty(B, S, C, dtype=torch.uint8, device=x.device)
+        with torch.cuda.device(x.device):
+            call("max_k", lib().pcops_max_k, ptr(x), 0 if x.dtype == torch.float32 else 1, B * S, K, C, ptr(out),
+                 ptr(arg), stream_of(x))
+        ctx.save_for_backward(arg)
+        ctx.K = K
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import call, lib, ptr, stream_of
+
+        (arg,) = ctx.saved_tensors
+        B, S, C = arg.shape
+        g = g.contiguous()
+        gx = torch.empty(B, S, ctx.K, C, dtype=g.dtype, device=g.device)
+        with torch.cuda.device(g.device):
+            call("max_k_grad", lib().pcops_max_k_grad, ptr(g), 0 if g.dtype == torch.float32 else 1, ptr(arg),
+                 B * S, ctx.K, C, ptr(gx), stream_of(g))
+        return gx
+
+
+def _max_k(t):
+    """max over dim 2 of a contiguous (B, S, K, C) tensor -> (B, S, C)."""
+    if (_MAXK and t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and t.shape[3] % 8 == 0
+            and t.shape[2] <= 255 and t.is_contiguous()):
+        return _MaxK.apply(t)
+    return torch.max(t, dim=2)[0]
+
+
 def max_over_neighbours(x):
     """torch.max(x, 3)[0] for a (B, C, S, K) neighbourhood tensor.  The 2-D
     convs produce it in channels_last memory (B, S, K, C), where torch's
     reduction over the strided last dim runs ~10x below HBM bandwidth; the
     same max (same values, same first-index argmax for the backward) is taken
-    over dim 2 of the contiguous (B, S, K, C) view instead."""
+    over dim 2 of the contiguous (B, S, K, C) view instead (pcops_max_k)."""
     if x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last):
-        return torch.max(x.permute(0, 2, 3, 1), dim=2)[0].permute(0, 2, 1).contiguous()
+        return _max_k(x.permute(0, 2, 3, 1)).permute(0, 2, 1).contiguous()
     return torch.max(x, 3)[0]
 
 
@@ -46,12 +87,13 @@ import os as _os
 
 # PCOPS_SA_FUSED=0: the unfused sample_and_group_knn path (A/B runs, parity tests)
 _SA_FUSED = _os.environ.get("PCOPS_SA_FUSED", "1") != "0"
+_MAXK = _os.environ.get("PCOPS_MAXK", "1") != "0"   # A/B switch: pcops_max_k for the neighbourhood max
 
 
 def max_over_neighbours_tokens(x):
     """max over K of a (B, C, S, K) channels_last tensor, returned as (B, S, C)."""
     if x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last):
-        return torch.max(x.permute(0, 2, 3, 1), dim=2)[0]
+        return _max_k(x.permute(0, 2, 3, 1))
     return torch.max(x, 3)[0].transpose(1, 2)
 
 # Which 1x1 convs run as GEMMs (A/B switch): sa | all (default) | edge | off.

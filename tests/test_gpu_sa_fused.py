@@ -10,6 +10,7 @@ import pytest
 import torch
 
 import svdformer_pointsea_amd.svdformer as S
+import svdformer_pointsea_amd.svdformer as S_mod
 
 pytestmark = pytest.mark.gpu
 
@@ -75,3 +76,24 @@ def test_sa_group_kernel_values(dev):
     assert torch.equal(out, ref)
     out16 = _SAGroup.apply(xyz, ctr, pts, idx, torch.bfloat16)
     assert torch.equal(out16, ref.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,S,K,C", [(4, 512, 16, 128), (2, 64, 8, 256), (3, 17, 5, 40)])
+def test_max_over_neighbours_kernel(dev, dt, B, S, K, C):
+    """pcops_max_k / _grad vs torch.max(dim=2) on (B, S, K, C): values bitwise,
+    gradient routed to the same (first) maximising k -- with many exact ties
+    (small-integer data) and a NaN."""
+    g = torch.Generator().manual_seed(K * C)
+    x = torch.randint(-4, 5, (B, S, K, C), generator=g).to(dt).to(dev)
+    x[0, 0, 2, 3] = float("nan")
+    xa = x.clone().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    out = S_mod._MaxK.apply(xa)
+    ref = torch.max(xb, dim=2)[0]
+    assert torch.equal(out.isnan(), ref.isnan())
+    assert torch.equal(torch.nan_to_num(out), torch.nan_to_num(ref))
+    go = torch.randn(out.shape, generator=g).to(dt).to(dev)
+    out.backward(go)
+    ref.backward(go)
+    assert torch.equal(xa.grad, xb.grad)
