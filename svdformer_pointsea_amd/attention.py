@@ -57,6 +57,8 @@ def _wgrad(g2, x2, wdt):
     weight dtype -- 2-4x faster at these shapes (tools/gemm_bench.py)."""
     T, Cout = g2.shape
     Cin = x2.shape[1]
+    if not _WGRAD_SPLITK:
+        return (g2.t() @ x2).to(wdt)
     S = 16 if Cout * Cin <= (2 << 20) else 4
     while S > 1 and (T % S or T // S < 2048):
         S //= 2
@@ -548,6 +550,7 @@ def block_sum(s, f):
 _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
 _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
 _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
+_WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switch: split-K weight gradients
 _PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
 _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnostic: fused sums in side-stream blocks too
 # linear11's bias sum inside the GELU backward: off by default -- 2 of 4 bench
