@@ -133,14 +133,20 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
     const uint64_t tied = __ballot(best == wmax);
     const int wl = (int)__builtin_ctzll(tied);  // lowest lane == smallest r in this wave
     // first slot of lane wl holding the maximum (in-thread strict '>' rule):
-    // pull lane wl's slots into SGPRs, search on the scalar unit
-    int wbi = PPT - 1;
+    // every lane finds its own first slot equal to wmax with VALU selects
+    // (two interleaved chains), then one readlane from lane wl -- the former
+    // PPT serial readlane + scalar compare steps were ~27 cycles each on the
+    // round's critical path
+    int wbi;
+    {
+      int b0 = PPT - 1, b1 = PPT - 1;
 #pragma unroll
-    for (int i = PPT - 2; i >= 0; --i) {
-      const int v = __builtin_amdgcn_readlane(tmp[i], wl);
-      wbi = (v == wmax) ? i : wbi;
+      for (int i = PPT - 2; i >= 0; i -= 2) {
+        b0 = (tmp[i] == wmax) ? i : b0;
+        if (i >= 1) b1 = (tmp[i - 1] == wmax) ? i - 1 : b1;
+      }
+      wbi = __builtin_amdgcn_readlane(min(b0, b1), wl);
     }
-    wbi = __builtin_amdgcn_readfirstlane(wbi);
     // uniform-index extraction (s_set_gpr_idx / movrel on a register vector)
     const float cx = px[wbi], cy = py[wbi], cz = pz[wbi];
     if (lane == wl) {
