@@ -124,7 +124,12 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
     int best = kNeverBits;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const int d = fbits(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz));
+      int d = fbits(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz));
+      // PPT >= 16: keep the distance chains scalar -- LLVM's SLP pass pairs
+      // them into v_pk_add/mul/fma_f32, which on gfx950 issue at half rate
+      // and add hazard s_nops (16384->2048: 2.78 -> 2.49 ms scalar); at small
+      // PPT the packed form measured slightly faster, so it is left there
+      if constexpr (PPT >= 16) asm volatile("" : "+v"(d));
       tmp[i] = min(d, tmp[i]);
       best = max(best, tmp[i]);
     }
