@@ -248,6 +248,33 @@ unsigned long long pcops_colsum_workspace_bytes(long long rows, int C);
 int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype, void *workspace,
                  unsigned long long workspace_bytes, pcops_stream_t stream);
 
+/* ---------------- BatchNorm (+ residual) (+ ReLU / LeakyReLU) on channels_last activations ----------------
+ * Replaces torch.nn.BatchNorm2d's forward / backward (MIOpen) together with the activation and
+ * residual add that follow it in the reference's encoders: ResNet BasicBlock (models/resnet.py:56-70,
+ * relu(bn1(conv1 x)), relu(bn2(conv2 .) + identity)), the SVFNet stem (models/SVDFormer.py:139-146),
+ * EdgeConv's bn + LeakyReLU(0.2) (models/model_utils.py:855-866) and PointSea's resnet18
+ * (models_PointSea/PointSea.py:37-61).  x is the (rows, C) memory of an NCHW tensor in channels_last
+ * order (rows = N*H*W), C % 8 == 0, C <= 512, rows*C/8 < 2^31, 16-byte aligned.
+ * dtype codes 0 fp32, 1 bf16 (x, y, dy, dx, dres share `dtype`; res has res_dtype); gamma, beta,
+ * running stats, save_mean / save_invstd fp32 (C).  act: 0 none, 1 ReLU, 2 LeakyReLU(slope).
+ * pcops_batchnorm_fwd: batch_stats = 1 (training): mean / biased var over the rows, saved as
+ *   save_mean / save_invstd = 1/sqrt(var + eps); running stats (either both NULL or both given)
+ *   updated with `momentum` and the unbiased var, as torch; batch_stats = 0 (eval): running stats.
+ *   y = act((x - mean) * invstd * gamma + beta (+ res)).
+ * pcops_batchnorm_bwd: dy is the gradient of y; y (the forward output) gives the activation's mask.
+ *   dx = the gradient of x; dres (optional) = the gradient of res (dy through the activation);
+ *   dgamma / dbeta (optional, C) overwritten.
+ * workspace (both): pcops_batchnorm_workspace_bytes(rows, C). */
+unsigned long long pcops_batchnorm_workspace_bytes(long long rows, int C);
+int pcops_batchnorm_fwd(const void *x, int dtype, const void *res, int res_dtype, long long rows, int C,
+                        const float *gamma, const float *beta, float *running_mean, float *running_var, float momentum,
+                        float eps, int batch_stats, int act, float slope, void *y, float *save_mean, float *save_invstd,
+                        void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+int pcops_batchnorm_bwd(const void *dy, const void *y, const void *x, int dtype, long long rows, int C,
+                        const float *gamma, const float *save_mean, const float *save_invstd, int batch_stats, int act,
+                        float slope, void *dx, void *dres, float *dgamma, float *dbeta, void *workspace,
+                        unsigned long long workspace_bytes, pcops_stream_t stream);
+
 /* ---------------- PCSA spectral gating (models/model_utils.py:358-430) ----------------
  * Per patch p (= b*S + s) of K neighbours x C channels stored [p][k][c] (the
  * channels_last memory order of the (B, C, S, K) conv output):

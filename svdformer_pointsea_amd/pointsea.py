@@ -30,6 +30,7 @@ from torch import nn
 from .attention import SDG_Decoder_PointSea, cross_attention, self_attention, to_tokens
 from .chamfer3D import chamfer_3DDist
 from ._lib import fork
+from .batchnorm import ACT_RELU, bn_act
 from .pointnet2_utils import furthest_point_sample, gather_operation
 from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin
 
@@ -63,7 +64,7 @@ class ResEncoder(nn.Module):
                 nn.init.constant_(m.bias, 0)
 
     def forward(self, input_view):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(input_view))))
+        x = self.maxpool(bn_act(self.conv1(input_view), self.bn1, ACT_RELU))
         return self.layer4(self.layer3(self.layer2(self.layer1(x))))
 
 

@@ -23,6 +23,7 @@ from .attention import SDG_Decoder, block_sum, cross_attention, linear, self_att
 from .chamfer3D import chamfer_3DDist
 from .model_utils import fps_subsample, group_local, sample_and_group_knn, sample_and_group_knn_cl
 from ._lib import fork
+from .batchnorm import ACT_RELU, bn_act, run_sequential
 from .pointnet2_utils import furthest_point_sample, gather_operation
 
 
@@ -321,8 +322,8 @@ class EdgeConv(nn.Module):
             central = torch.zeros(B, C, N, 1, device=inputs.device, dtype=inputs.dtype)
             neigh = inputs.unsqueeze(-1)
         feature = torch.cat((central - neigh, central), dim=1).contiguous(memory_format=torch.channels_last)
-        for m in self.conv:
-            feature = conv1x1(feature, m, "edge") if isinstance(m, nn.Conv2d) else m(feature)
+        # 1x1 convs as GEMMs, each BatchNorm2d + LeakyReLU pair as one bn_act
+        feature = run_sequential(self.conv, feature, lambda t, m: conv1x1(t, m, "edge"))
         return max_over_neighbours(feature)
 
 
@@ -363,10 +364,10 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + identity)
+        # bn + (residual) + relu fused on libpcops (batchnorm.bn_act; torch's modules when not fusable)
+        identity = x if self.downsample is None else run_sequential(self.downsample, x)
+        out = bn_act(self.conv1(x), self.bn1, ACT_RELU)
+        return bn_act(self.conv2(out), self.bn2, ACT_RELU, residual=identity)
 
 
 def _resnet_layers(feature_size=16, layers=(2, 2, 2, 2)):
@@ -517,7 +518,7 @@ class SVFNet(nn.Module):
     def forward(self, points, depth):
         batch_size, _, N = points.size()
         depth = depth.contiguous(memory_format=torch.channels_last)
-        f_v = self.img_feature_extractor(depth).view(batch_size, 3, -1).transpose(1, 2).contiguous()
+        f_v = run_sequential(self.img_feature_extractor, depth).view(batch_size, 3, -1).transpose(1, 2).contiguous()
         f_p = self.point_feature_extractor(points)
         view_point = self.view_point.expand(batch_size, 3, 3)
         view_feature = self.posmlp(view_point).permute(2, 0, 1)
