@@ -20,8 +20,10 @@ import svdformer_pointsea_amd.svdformer as S
 pytestmark = pytest.mark.gpu
 
 
-def _ref(x, res, w, b, rm, rv, training, mom, eps, act, slope):
-    """float64 BatchNorm2d (+res) (+act); returns y and the updated running stats."""
+def _ref(x, res, w, b, rm, rv, training, mom, eps, act, slope, round16=False):
+    """float64 BatchNorm2d (+res) (+act); returns y and the updated running stats.
+    round16: the BN output is rounded to bf16 before the residual add (torch's bf16
+    BatchNorm output as stored; straight-through for the gradient)."""
     xd = x.double()
     C = x.shape[1]
     if training:
@@ -36,6 +38,8 @@ def _ref(x, res, w, b, rm, rv, training, mom, eps, act, slope):
     y = (xd - mean.view(1, C, 1, 1)) / torch.sqrt(var.view(1, C, 1, 1) + eps) * w.double().view(1, C, 1, 1) \
         + b.double().view(1, C, 1, 1)
     if res is not None:
+        if round16:
+            y = y + (y.to(torch.bfloat16).double() - y).detach()
         y = y + res.double()
     _ref.pre = y.detach()
     if act == BN.ACT_RELU:
@@ -84,7 +88,7 @@ def test_bn_act_train_vs_float64(dev, shape, dtype, act, res):
     rr = r.double().requires_grad_(True) if res else None
     wr = bn.weight.detach().double().requires_grad_(True)
     br = bn.bias.detach().double().requires_grad_(True)
-    yr, rm2, rv2 = _ref(xr, rr, wr, br, rm0, rv0, True, 0.1, 1e-5, act, 0.2)
+    yr, rm2, rv2 = _ref(xr, rr, wr, br, rm0, rv0, True, 0.1, 1e-5, act, 0.2, round16=dtype == torch.bfloat16)
     yr.backward(dy.double())
     # elementwise gradient checks skip pre-activations within 1e-4 of the kink, where
     # fp32 vs float64 rounding may pick the other side of the activation
@@ -162,15 +166,6 @@ def _block_grads(mod, x, enabled, monkeypatch, amp):
     return y.float(), xg.grad.float(), grads, bufs
 
 
-def _close_mostly(a, b, atol, rtol, max_frac):
-    """assert_close except for at most max_frac of the elements: under bf16 autocast one
-    ReLU whose pre-activation rounds to the other side of zero (fp32 BN arithmetic in a
-    different order than MIOpen's) moves that element's gradient by a full dy, and the
-    next conv's dgrad spreads it to its neighbourhood."""
-    bad = ((a - b).abs() > atol + rtol * b.abs()).float().mean().item()
-    assert bad <= max_frac, f"{bad:.4%} of elements outside atol={atol} rtol={rtol}"
-
-
 @pytest.mark.parametrize("amp", [False, True])
 @pytest.mark.parametrize("down", [False, True])
 def test_basic_block_fused_vs_torch(dev, monkeypatch, amp, down):
@@ -198,10 +193,25 @@ def test_basic_block_fused_vs_torch(dev, monkeypatch, amp, down):
         for k in ba:
             torch.testing.assert_close(ba[k], bb[k], atol=1e-5, rtol=1e-5)
     else:
-        _close_mostly(ya, yb, 1e-2, 2 ** -7, 1e-3)
-        _close_mostly(gxa, gxb, 5e-2, 2e-2, 2e-2)
-        for k in ga:
-            torch.testing.assert_close(ga[k], gb[k], atol=0.5, rtol=5e-2)
+        # bf16: MIOpen's bf16 BatchNorm and this one round differently (its statistics are not
+        # exact), and one ReLU flipped by a bf16 ulp moves a gradient element by a full dy that
+        # the next conv spreads -- so both are measured against the float64 block, and the
+        # fused path must be at least as accurate as torch's
+        blk64 = copy.deepcopy(blk).double().cpu()
+        x64 = x.detach().double().cpu().requires_grad_(True)
+        monkeypatch.setattr(BN, "ENABLED", False)
+        y64 = blk64(x64)
+        dy = torch.randn(y64.shape, generator=torch.Generator().manual_seed(1)).to(torch.bfloat16).double()
+        (y64 * dy).sum().backward()
+        g64 = {n: p.grad for n, p in blk64.named_parameters() if p.grad is not None}
+
+        def rel(a, ref):
+            return ((a.double().cpu() - ref).norm() / ref.norm()).item()
+
+        for name, a, b, r in [("y", ya, yb, y64.detach()), ("dx", gxa, gxb, x64.grad)] + \
+                [(k, ga[k], gb[k], g64[k]) for k in ga]:
+            ea, eb = rel(a, r), rel(b, r)
+            assert ea <= 1.25 * eb + 2e-3, f"{name}: fused rel err {ea:.3g} vs torch {eb:.3g}"
         for k in ba:
             torch.testing.assert_close(ba[k], bb[k], atol=1e-3, rtol=1e-3)
 
