@@ -618,11 +618,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     progress(f"timing {args.steps} steps")
+    loss_hist = [loss_acc.clone()]   # running loss after the warm-up and after each timed step (no host sync)
     t0 = time.perf_counter()
     host = 0.0  # time the host spends issuing a step (launches are asynchronous)
     for _ in range(args.steps):
         h0 = time.perf_counter()
         step()
+        loss_hist.append(loss_acc.clone())
         host += time.perf_counter() - h0
     if use_dist:
         dist.barrier()
@@ -643,6 +645,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     if not math.isfinite(loss_acc.item()):
+        # where it started: the first non-finite running loss (0 = warm-up), and which
+        # flat buffers / parameters carry non-finite values now
+        hist = torch.stack(loss_hist).cpu()
+        bad = [i for i, v in enumerate(hist.tolist()) if not math.isfinite(v)]
+        names = [n for n, q in model.named_parameters()
+                 if not torch.isfinite(q.detach()).all() or (q.grad is not None and not torch.isfinite(q.grad).all())]
+        progress(f"non-finite running loss from snapshot {bad[0]} of {len(hist)} (0 = after warm-up); "
+                 f"master finite {bool(torch.isfinite(fp.flat).all())}, grad finite {bool(torch.isfinite(fp.grad).all())}; "
+                 f"{len(names)} parameters non-finite, first: {names[:6]}")
         raise RuntimeError("non-finite loss in the timed steps")
 
     fp32_leg = None

@@ -275,6 +275,22 @@ int pcops_batchnorm_bwd(const void *dy, const void *y, const void *x, int dtype,
                         float slope, void *dx, void *dres, float *dgamma, float *dbeta, void *workspace,
                         unsigned long long workspace_bytes, pcops_stream_t stream);
 
+/* ---------------- 3x3 convolution, stride 1, pad 1, no bias, on channels_last bf16 ----------------
+ * The ResNet BasicBlock convs of SVDFormer's image encoder (models/resnet.py:36-70 via
+ * models/SVDFormer.py:139-146), replacing torch.nn.Conv2d's MIOpen forward / backward.
+ * x, y: (N, H, W, C) bf16 (an NCHW tensor in channels_last memory), C in {16, 32}, 16-byte aligned.
+ * pcops_conv3x3_fwd: y[n][h][w][co] = sum_{kh,kw,ci} x[n][h+kh-1][w+kw-1][ci] * w[co][kh][kw][ci]
+ *   (w: OHWI bf16, zero padding).  The input gradient of the same conv is
+ *   pcops_conv3x3_fwd(dy, w', dx) with w'[ci][kh][kw][co] = w[co][ci][2-kh][2-kw].
+ * pcops_conv3x3_wgrad: dw[co][ci][kh][kw] = sum_{n,h,w} dy[n][h][w][co] * x[n][h+kh-1][w+kw-1][ci],
+ *   written as fp32 (dw_dtype 0) or bf16 (1), in OIHW (dw_ohwi 0) or OHWI (1) memory order;
+ *   fp32 accumulation, block partials summed in a fixed order.
+ *   workspace: pcops_conv3x3_wgrad_workspace_bytes(C). */
+int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int W, int C, void *y, pcops_stream_t stream);
+unsigned long long pcops_conv3x3_wgrad_workspace_bytes(int C);
+int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, int W, int C, void *dw, int dw_dtype,
+                        int dw_ohwi, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+
 /* ---------------- PCSA spectral gating (models/model_utils.py:358-430) ----------------
  * Per patch p (= b*S + s) of K neighbours x C channels stored [p][k][c] (the
  * channels_last memory order of the (B, C, S, K) conv output):

@@ -66,6 +66,9 @@ _SIGS = {
     "pcops_batchnorm_workspace_bytes": (ULL, [LL, I]),
     "pcops_batchnorm_fwd": (I, [P, I, P, I, LL, I, P, P, P, P, F, F, I, I, F, P, P, P, P, ULL, P]),
     "pcops_batchnorm_bwd": (I, [P, P, P, I, LL, I, P, P, P, I, I, F, P, P, P, P, P, ULL, P]),
+    "pcops_conv3x3_fwd": (I, [P, P, I, I, I, I, P, P]),
+    "pcops_conv3x3_wgrad_workspace_bytes": (ULL, [I]),
+    "pcops_conv3x3_wgrad": (I, [P, P, I, I, I, I, P, I, I, P, ULL, P]),
     "pcops_pcsa_forward": (I, [P, I, P, I, P, I, I, I, P, P]),
     "pcops_pcsa_backward": (I, [P, I, P, I, P, I, P, I, I, I, P, P, P]),
     "pcops_points2depth_workspace_bytes": (ULL, [I, I, I, I]),

@@ -1,0 +1,77 @@
+"""3x3 / stride 1 / pad 1 / bias-free nn.Conv2d on channels_last bf16 activations
+through libpcops (pcops_conv3x3_fwd / _wgrad, csrc/conv.hip): the ResNet
+BasicBlock convs of SVDFormer's image encoder (models/resnet.py:36-70 via
+models/SVDFormer.py:139-146; C = 16 at 224x224 and 32 at 112x112 for the 96
+depth images of a PCN batch), where MIOpen's NHWC kernels ran 2.5-6x below
+HBM speed.  Other convs (strides, other channel counts, fp32 inputs) stay on
+torch's nn.Conv2d.  The module and its state_dict are unchanged.
+"""
+import os
+
+import torch
+from torch import nn
+
+from ._lib import Workspace, call, lib, ptr, stream_of
+
+# PCOPS_CONV3X3=0: torch's nn.Conv2d (MIOpen) for every conv (A/B runs, parity tests)
+ENABLED = os.environ.get("PCOPS_CONV3X3", "1") != "0"
+_CHANNELS = (16, 32)
+
+
+def _ohwi(w):
+    """(Co, Ci, 3, 3) -> bf16 [co][kh][kw][ci] (a view when w is already channels_last bf16)."""
+    return w.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        N, C, H, W = x.shape
+        y = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        with torch.cuda.device(x.device):
+            call("conv3x3_fwd", lib().pcops_conv3x3_fwd, ptr(x), ptr(_ohwi(w)), N, H, W, C, ptr(y), stream_of(x))
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        N, C, H, W = x.shape
+        gy = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        gx = gw = None
+        with torch.cuda.device(x.device):
+            if ctx.needs_input_grad[0]:
+                # stride-1 input gradient: the same conv of dy with w'[ci][kh][kw][co] = w[co][ci][2-kh][2-kw]
+                wt = w.to(torch.bfloat16).flip(2, 3).permute(1, 2, 3, 0).contiguous()
+                gx = torch.empty_like(x)
+                call("conv3x3_dgrad", lib().pcops_conv3x3_fwd, ptr(gy), ptr(wt), N, H, W, C, ptr(gx), stream_of(x))
+            if ctx.needs_input_grad[1]:
+                gw = torch.empty_like(w)   # w's dtype and memory order (OIHW or channels_last OHWI)
+                ohwi = int(w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous())
+                if not (ohwi or w.is_contiguous()):
+                    gw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
+                nbytes = lib().pcops_conv3x3_wgrad_workspace_bytes(C)
+                ws = Workspace.get(x.device, nbytes)
+                call("conv3x3_wgrad", lib().pcops_conv3x3_wgrad, ptr(x), ptr(gy), N, H, W, C, ptr(gw),
+                     0 if w.dtype == torch.float32 else 1, ohwi, ptr(ws), nbytes, stream_of(x))
+        return gx, gw
+
+
+def eligible(x, conv):
+    if not (ENABLED and isinstance(conv, nn.Conv2d) and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16):
+        return False
+    C = x.shape[1]
+    return (conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"
+            and C in _CHANNELS and conv.in_channels == C and conv.out_channels == C
+            and conv.weight.dtype in (torch.float32, torch.bfloat16)
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+
+
+def conv3x3(x, conv, weight=None):
+    """conv(x) for an nn.Conv2d; libpcops when eligible (see module doc), torch otherwise.
+    `weight` overrides conv.weight (e.g. a bf16 shadow)."""
+    w = conv.weight if weight is None else weight
+    if eligible(x, conv) and w.dtype in (torch.float32, torch.bfloat16):
+        return _Conv3x3.apply(x, w)
+    return conv(x)

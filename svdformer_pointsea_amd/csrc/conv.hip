@@ -1,0 +1,284 @@
+// 3x3 / stride 1 / pad 1 convolution of channels_last (NHWC) bf16 activations
+// on MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulation): the ResNet BasicBlock
+// convs of SVDFormer's image encoder (models/resnet.py:36-70 via
+// models/SVDFormer.py:139-146: C = 16 at 224x224, 32 at 112x112; 96 images per
+// PCN batch), where MIOpen's NHWC kernels ran 2.5-6x below HBM speed.
+//
+// forward / input gradient (implicit GEMM, one kernel):
+//   y[p][co] = sum_{tap, ci} x[p + off(tap)][ci] * w[co][tap][ci]      (w: OHWI bf16)
+//   as D = A . B with A = w (M = co, K = (tap, ci)) held in registers and
+//   B = the input window (K x N = pixels) read from an LDS image of the block's
+//   (4 + 2) x (64 + 2) input rows: lane l reads the 8 channels k = 8(l>>4)..+7 of
+//   pixel l&15 at one tap -- one ds_read_b128, no transpose.  The input gradient
+//   of a stride-1 conv is the same product on dy with w'[ci][tap][co] =
+//   w[co][ci][8 - tap] (flipped, transposed: built on the host).
+// weight gradient:
+//   dW[co][tap][ci] = sum_p dy[p][co] * x[p + off(tap)][ci]
+//   K = pixels: both operands are read with ds_read_b64_tr_b16 (4 pixels x 16
+//   channels per 16-lane group, delivered channel-major) from LDS images of the
+//   dy tile and the haloed x tile; one A fragment serves the 9 taps.  Each block
+//   loops over tiles, keeps its partial dW in registers and writes it once; a
+//   second kernel sums the block partials in a fixed order (deterministic).
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTH = 4;        // output rows per tile (one per wave)
+constexpr int kTW = 64;       // output columns per tile
+constexpr int kLW = kTW + 2;  // haloed input tile columns
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8 &a, const bf16x8 &b, const f32x4 &c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// stage the haloed input tile rows h0-1 .. h0+kTH, cols w0-1 .. w0+kTW of image n
+// (zeros outside the image) as [row][col][C] bf16
+template <int C>
+__device__ __forceinline__ void stage_halo(__bf16 *tile, const __bf16 *__restrict__ x, int n, int h0, int w0, int H,
+                                           int W) {
+  constexpr int VPP = C / 8;
+  for (int i = threadIdx.x; i < (kTH + 2) * kLW * VPP; i += 256) {
+    const int v = i % VPP, pc = i / VPP, c = pc % kLW, r = pc / kLW;
+    const int hh = h0 - 1 + r, ww = w0 - 1 + c;
+    bf16x8 val = {};
+    if (hh >= 0 && hh < H && ww >= 0 && ww < W)
+      val = *reinterpret_cast<const bf16x8 *>(x + (((long long)n * H + hh) * W + ww) * C + 8 * v);
+    *reinterpret_cast<bf16x8 *>(tile + (r * kLW + c) * C + 8 * v) = val;
+  }
+}
+
+// ---------------------------------------------------------------- forward / dgrad
+template <int CI, int CO>
+__global__ __launch_bounds__(256) void conv3x3_fwd_kernel(const __bf16 *__restrict__ x,
+                                                          const __bf16 *__restrict__ w, __bf16 *__restrict__ y,
+                                                          int H, int W) {
+  constexpr int KC = (9 * CI + 31) / 32;  // K chunks of 32 over (tap, ci); the tail has zero weights
+  constexpr int MT = CO / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 tile[(kTH + 2) * kLW * CI];
+  const int n = blockIdx.z, h0 = blockIdx.y * kTH, w0 = blockIdx.x * kTW;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l >> 4, i16 = l & 15;
+  stage_halo<CI>(tile, x, n, h0, w0, H, W);
+  bf16x8 a[MT][KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int k0 = 32 * c + 8 * g, tap = k0 / CI, ci0 = k0 % CI;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      a[mt][c] = tap < 9 ? *reinterpret_cast<const bf16x8 *>(w + ((16 * mt + i16) * 9 + tap) * CI + ci0) : bf16x8{};
+  }
+  __syncthreads();
+  const int orow = h0 + wv;
+#pragma unroll
+  for (int nt = 0; nt < kTW / 16; ++nt) {
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int pc = 16 * nt + i16;  // output column in the tile (this lane's B column)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int k0 = 32 * c + 8 * g;
+      const int tap = k0 / CI < 9 ? k0 / CI : 8;  // K tail: finite data against zero weights
+      const int ci0 = k0 % CI, dh = tap / 3, dw = tap % 3;
+      const bf16x8 b = *reinterpret_cast<const bf16x8 *>(tile + ((wv + dh) * kLW + pc + dw) * CI + ci0);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(a[mt][c], b, acc[mt]);
+    }
+    const int ow = w0 + pc;
+    if (orow < H && ow < W) {
+      __bf16 *yp = y + (((long long)n * H + orow) * W + ow) * CO + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[mt][r];
+        *reinterpret_cast<bf16x4 *>(yp + 16 * mt) = o;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- weight gradient
+// grid: G blocks looping over the N * ceil(H/kTH) * ceil(W/kTW) tiles; partial
+// dW per block in part[block][co][tap][ci] (fp32)
+template <int CI, int CO>
+__global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(const __bf16 *__restrict__ x,
+                                                            const __bf16 *__restrict__ dy, int N, int H, int W,
+                                                            float *__restrict__ part) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int MT = CO / 16, NT = CI / 16;
+  // one LDS arena: the x / dy images while looping, the 9*CO*CI fp32 block partial at the end
+  constexpr int kXT = (kTH + 2) * kLW * CI, kGT = kTH * kTW * CO, kE = 9 * CO * CI;
+  constexpr int kBytes = (2 * (kXT + kGT) > 4 * kE ? 2 * (kXT + kGT) : 4 * kE);
+  __shared__ float4 arena[(kBytes + 15) / 16];
+  __bf16 *xt = reinterpret_cast<__bf16 *>(arena);
+  __bf16 *gt = xt + kXT;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l >> 4, i16 = l & 15, q = i16 >> 2, p = i16 & 3;
+  const int tw = (W + kTW - 1) / kTW, th = (H + kTH - 1) / kTH;
+  const long long tiles = (long long)N * th * tw;
+  f32x4 acc[9][MT][NT];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[t][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int bx = (int)(t % tw);
+    const long long r = t / tw;
+    const int by = (int)(r % th), n = (int)(r / th);
+    const int h0 = by * kTH, w0 = bx * kTW;
+    __syncthreads();  // the previous tile's reads are done
+    stage_halo<CI>(xt, x, n, h0, w0, H, W);
+    constexpr int VPO = CO / 8;
+    for (int i = threadIdx.x; i < kTH * kTW * VPO; i += 256) {
+      const int v = i % VPO, pc = i / VPO, c = pc % kTW, rr = pc / kTW;
+      const int hh = h0 + rr, ww = w0 + c;
+      bf16x8 val = {};
+      if (hh < H && ww < W) val = *reinterpret_cast<const bf16x8 *>(dy + (((long long)n * H + hh) * W + ww) * CO + 8 * v);
+      *reinterpret_cast<bf16x8 *>(gt + (rr * kTW + c) * CO + 8 * v) = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kc = 0; kc < kTW / 32; ++kc) {
+      // pixels 32kc + 8g + (0..3 | 4..7) of row wv; lane 4q+p addresses row q, channels 4p..4p+3
+      const int px0 = 32 * kc + 8 * g + q;
+      bf16x8 a[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const __bf16 *base = gt + (wv * kTW + px0) * CO + 16 * mt + 4 * p;
+        const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)base);
+        const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(base + 4 * CO));
+        a[mt] = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1, 2, 3,
+                                        4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dh = tap / 3, dw = tap % 3;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const __bf16 *base = xt + ((wv + dh) * kLW + px0 + dw) * CI + 16 * nt + 4 * p;
+          const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)base);
+          const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(base + 4 * CI));
+          const bf16x8 b = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0,
+                                                   1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[tap][mt][nt] = mfma16(a[mt], b, acc[tap][mt][nt]);
+        }
+      }
+    }
+  }
+  // reduce the four waves' partials through LDS (reusing the x image), then one
+  // store per element: part[block][co][tap][ci]
+  __syncthreads();
+  float *red = reinterpret_cast<float *>(arena);
+  constexpr int E = kE;
+  for (int i = threadIdx.x; i < E; i += 256) red[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (wv == s) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int co = 16 * mt + 4 * g + r, ci = 16 * nt + i16;
+              red[(co * 9 + tap) * CI + ci] += acc[tap][mt][nt][r];
+            }
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < E; i += 256) part[(long long)blockIdx.x * E + i] = red[i];
+#endif
+}
+
+// dw = sum over blocks of part[b][co][tap][ci], written in the weight's memory
+// order -- OIHW [co][ci][kh][kw] or channels_last OHWI [co][kh][kw][ci] -- as fp32
+// or bf16 (the dtype of the weight it is the gradient of)
+__global__ __launch_bounds__(256) void conv3x3_wgrad_final_kernel(const float *__restrict__ part, int blocks, int CO,
+                                                                  int CI, void *__restrict__ out, int odt,
+                                                                  int ohwi) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int E = 9 * CO * CI;
+  if (e >= E) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = 0;
+  for (; b + 3 < blocks; b += 4) {
+    s0 += part[(long long)b * E + e];
+    s1 += part[(long long)(b + 1) * E + e];
+    s2 += part[(long long)(b + 2) * E + e];
+    s3 += part[(long long)(b + 3) * E + e];
+  }
+  for (; b < blocks; ++b) s0 += part[(long long)b * E + e];
+  const float v = (s0 + s1) + (s2 + s3);
+  const int co = e / (9 * CI), rem = e - co * 9 * CI, tap = rem / CI, ci = rem - tap * CI;
+  const int o = ohwi ? e : (co * CI + ci) * 9 + tap;
+  if (odt == 0)
+    reinterpret_cast<float *>(out)[o] = v;
+  else
+    reinterpret_cast<__bf16 *>(out)[o] = (__bf16)v;
+}
+
+int wgrad_blocks(int C) { return C <= 16 ? 1024 : 512; }
+
+bool conv_ok(int N, int H, int W, int C) { return N > 0 && H > 0 && W > 0 && (C == 16 || C == 32); }
+
+}  // namespace
+
+extern "C" int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int W, int C, void *y,
+                                 pcops_stream_t stream) {
+  if (N < 0 || H < 0 || W < 0) return PCOPS_ERR_INVALID;
+  if (N == 0 || H == 0 || W == 0) return PCOPS_OK;
+  if (!conv_ok(N, H, W, C)) return PCOPS_ERR_UNSUPPORTED;
+  if (!x || !w || !y) return PCOPS_ERR_INVALID;
+  const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, N);
+  hipStream_t s = (hipStream_t)stream;
+  if (C == 16)
+    hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16>), grid, dim3(256), 0, s, (const __bf16 *)x, (const __bf16 *)w,
+                       (__bf16 *)y, H, W);
+  else
+    hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32>), grid, dim3(256), 0, s, (const __bf16 *)x, (const __bf16 *)w,
+                       (__bf16 *)y, H, W);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" unsigned long long pcops_conv3x3_wgrad_workspace_bytes(int C) {
+  if (C != 16 && C != 32) return 0;
+  return (unsigned long long)wgrad_blocks(C) * 9 * C * C * sizeof(float);
+}
+
+extern "C" int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, int W, int C, void *dw, int dw_dtype,
+                                   int dw_ohwi, void *workspace, unsigned long long workspace_bytes,
+                                   pcops_stream_t stream) {
+  if (N < 0 || H < 0 || W < 0 || !dw || (dw_dtype != 0 && dw_dtype != 1)) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 0 || H == 0 || W == 0) {
+    if (hipMemsetAsync(dw, 0, (dw_dtype == 0 ? 4 : 2) * 9 * C * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!conv_ok(N, H, W, C)) return PCOPS_ERR_UNSUPPORTED;
+  if (!x || !dy) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_conv3x3_wgrad_workspace_bytes(C)) return PCOPS_ERR_WORKSPACE;
+  const int G = wgrad_blocks(C);
+  float *part = (float *)workspace;
+  if (C == 16)
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<16, 16>), dim3(G), dim3(256), 0, s, (const __bf16 *)x,
+                       (const __bf16 *)dy, N, H, W, part);
+  else
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<32, 32>), dim3(G), dim3(256), 0, s, (const __bf16 *)x,
+                       (const __bf16 *)dy, N, H, W, part);
+  hipLaunchKernelGGL(conv3x3_wgrad_final_kernel, dim3((9 * C * C + 255) / 256), dim3(256), 0, s, part, G, C, C, dw, dw_dtype,
+                     dw_ohwi);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}

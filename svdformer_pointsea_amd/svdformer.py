@@ -24,6 +24,7 @@ from .chamfer3D import chamfer_3DDist
 from .model_utils import fps_subsample, group_local, sample_and_group_knn, sample_and_group_knn_cl
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act, run_sequential
+from .conv import conv3x3
 from .pointnet2_utils import furthest_point_sample, gather_operation
 
 
@@ -365,9 +366,10 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         # bn + (residual) + relu fused on libpcops (batchnorm.bn_act; torch's modules when not fusable)
+        # 3x3 stride-1 convs at C = 16 / 32 on libpcops MFMA kernels (conv.conv3x3; MIOpen otherwise)
         identity = x if self.downsample is None else run_sequential(self.downsample, x)
-        out = bn_act(self.conv1(x), self.bn1, ACT_RELU)
-        return bn_act(self.conv2(out), self.bn2, ACT_RELU, residual=identity)
+        out = bn_act(conv3x3(x, self.conv1), self.bn1, ACT_RELU)
+        return bn_act(conv3x3(out, self.conv2), self.bn2, ACT_RELU, residual=identity)
 
 
 def _resnet_layers(feature_size=16, layers=(2, 2, 2, 2)):

@@ -41,8 +41,11 @@ run_stage() {
                   2> "$OUT/bench_fp32.err" ;;
     trace) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
              python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32-leg > "$OUT/bench_traced.json" \
-             2> "$OUT/trace.err" &&
-           find "$OUT/trace" -name '*kernel_trace.csv' -exec gzip -9 {} + ;;   # keep the merge-back small
+             2> "$OUT/trace.err"
+           rc=$?
+           find "$OUT/trace" -name '*kernel_trace.csv' -exec gzip -9 {} +   # keep the merge-back small
+           [ $rc -eq 0 ] || tail -30 "$OUT/trace.err"
+           return $rc ;;
     pmc_traffic)
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
         -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
