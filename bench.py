@@ -207,6 +207,25 @@ def kernel_work(name, a):
     if name == "chamfer_3D.backward":  # xyz1, xyz2, B, n, m: per point read xyz, partner xyz, grad, idx; write own
         B, n, m = a[2], a[3], a[4]       # grad, scatter-add the partner's (12 + 12 + 4 + 4 + 12 + 12 B)
         return float(56 * B * (n + m)), "GB/s", HBM_PEAK, "hbm"
+    if name == "batchnorm_fwd":  # x, dt, res, rdt, rows, C, ..., batch_stats (12): x read by the stats pass
+        n, e = a[4] * a[5], es(a[1])   # and the apply pass (two passes: the statistics precede the
+        return float(n * e * (2 if a[12] else 1) + (n * es(a[3]) if a[2] else 0) + n * e), "GB/s", HBM_PEAK, "hbm"
+    if name == "batchnorm_bwd":  # dy, y, x, dt, rows, C, ..., act (10), ..., dres (13): dy / y / x read by the
+        n, e = a[4] * a[5], es(a[3])   # reduce and the apply pass, dx (+ dres) written once
+        rd = 3 if a[10] else 2
+        return float(2 * rd * n * e + n * e * (2 if a[13] else 1)), "GB/s", HBM_PEAK, "hbm"
+    if name in ("conv3x3_fwd", "conv3x3_dgrad"):  # x, w, N, H, W, C, y: read the input, write the output once
+        return float(2 * 2 * a[2] * a[3] * a[4] * a[5]), "GB/s", HBM_PEAK, "hbm"
+    if name == "conv3x3_wgrad":  # x, dy, N, H, W, C: read both activations once
+        return float(2 * 2 * a[2] * a[3] * a[4] * a[5]), "GB/s", HBM_PEAK, "hbm"
+    if name == "add":            # a, adt, b, bdt, out, odt, n
+        return float(a[6] * (es(a[1]) + es(a[3]) + es(a[5]))), "GB/s", HBM_PEAK, "hbm"
+    if name == "max_k":          # x, dt, rows, K, C, out, arg: read K rows, write the max + a uint8 argmax
+        return float(a[2] * a[4] * ((a[3] + 1) * es(a[1]) + 1)), "GB/s", HBM_PEAK, "hbm"
+    if name == "max_k_grad":     # g, dt, arg, rows, K, C, gx: read g + argmax, write the K rows
+        return float(a[3] * a[5] * ((a[4] + 1) * es(a[1]) + 1)), "GB/s", HBM_PEAK, "hbm"
+    if name == "gelu_bwd":       # dy, u, dt, rows, C, du: read dy and u, write du
+        return float(3 * a[3] * a[4] * es(a[2])), "GB/s", HBM_PEAK, "hbm"
     if name == "points2depth":   # points, rot, trans, B, N, V, H, W: read the cloud, accumulate 8 B / pixel
         B, N, V, H, W = a[3], a[4], a[5], a[6], a[7]  # (written + re-read), write the image
         return float(12 * B * N + 20 * B * V * H * W), "GB/s", HBM_PEAK, "hbm"

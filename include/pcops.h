@@ -264,12 +264,14 @@ int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, i
  * pcops_batchnorm_bwd: dy is the gradient of y; y (the forward output) gives the activation's mask.
  *   dx = the gradient of x; dres (optional) = the gradient of res (dy through the activation);
  *   dgamma / dbeta (optional, C) overwritten.
- * workspace (both): pcops_batchnorm_workspace_bytes(rows, C). */
+ * workspace (both): pcops_batchnorm_workspace_bytes(rows, C).
+ * num_batches_tracked (optional, int64): incremented by the training forward when running stats are given. */
 unsigned long long pcops_batchnorm_workspace_bytes(long long rows, int C);
 int pcops_batchnorm_fwd(const void *x, int dtype, const void *res, int res_dtype, long long rows, int C,
                         const float *gamma, const float *beta, float *running_mean, float *running_var, float momentum,
                         float eps, int batch_stats, int act, float slope, void *y, float *save_mean, float *save_invstd,
-                        void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+                        void *workspace, unsigned long long workspace_bytes, long long *num_batches_tracked,
+                        pcops_stream_t stream);
 int pcops_batchnorm_bwd(const void *dy, const void *y, const void *x, int dtype, long long rows, int C,
                         const float *gamma, const float *save_mean, const float *save_invstd, int batch_stats, int act,
                         float slope, void *dx, void *dres, float *dgamma, float *dbeta, void *workspace,

@@ -64,7 +64,7 @@ _SIGS = {
     "pcops_colsum_workspace_bytes": (ULL, [LL, I]),
     "pcops_colsum": (I, [P, I, LL, I, P, I, P, ULL, P]),
     "pcops_batchnorm_workspace_bytes": (ULL, [LL, I]),
-    "pcops_batchnorm_fwd": (I, [P, I, P, I, LL, I, P, P, P, P, F, F, I, I, F, P, P, P, P, ULL, P]),
+    "pcops_batchnorm_fwd": (I, [P, I, P, I, LL, I, P, P, P, P, F, F, I, I, F, P, P, P, P, ULL, P, P]),
     "pcops_batchnorm_bwd": (I, [P, P, P, I, LL, I, P, P, P, I, I, F, P, P, P, P, P, ULL, P]),
     "pcops_conv3x3_fwd": (I, [P, P, I, I, I, I, P, P]),
     "pcops_conv3x3_wgrad_workspace_bytes": (ULL, [I]),

@@ -32,7 +32,7 @@ def _rows_c(x):
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, rmean, rvar, batch_stats, momentum, eps, act, slope):
+    def forward(ctx, x, res, weight, bias, rmean, rvar, nbt, batch_stats, momentum, eps, act, slope):
         rows, C = _rows_c(x)
         y = torch.empty_like(x)  # channels_last strides preserved
         smean = torch.empty(C, dtype=torch.float32, device=x.device)
@@ -43,7 +43,7 @@ class _BNAct(torch.autograd.Function):
             call("batchnorm_fwd", lib().pcops_batchnorm_fwd, ptr(x), _DT[x.dtype], ptr(res),
                  _DT[res.dtype] if res is not None else 0, rows, C, ptr(weight), ptr(bias), ptr(rmean), ptr(rvar),
                  float(momentum), float(eps), int(batch_stats), act, float(slope), ptr(y), ptr(smean), ptr(sinv),
-                 ptr(ws), nbytes, stream_of(x))
+                 ptr(ws), nbytes, ptr(nbt), stream_of(x))
         ctx.save_for_backward(x, y if act != ACT_NONE else None, weight, smean, sinv)
         ctx.cfg = (batch_stats, act, slope, res is not None)
         return y
@@ -65,7 +65,7 @@ class _BNAct(torch.autograd.Function):
             call("batchnorm_bwd", lib().pcops_batchnorm_bwd, ptr(gy), ptr(y), ptr(x), _DT[x.dtype], rows, C,
                  ptr(weight), ptr(smean), ptr(sinv), int(batch_stats), act, float(slope), ptr(dx), ptr(dres),
                  ptr(dgamma), ptr(dbeta), ptr(ws), nbytes, stream_of(x))
-        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None
 
 
 def _fusable(x, bn, residual):
@@ -103,11 +103,11 @@ def bn_act(x, bn, act=ACT_NONE, slope=0.0, residual=None):
         return _activation(out, act, slope)
     batch_stats = bn.training or bn.running_mean is None
     update = bn.training and bn.running_mean is not None
-    if update:
-        bn.num_batches_tracked.add_(1)
     rm = bn.running_mean if (update or not batch_stats) else None
     rv = bn.running_var if (update or not batch_stats) else None
-    return _BNAct.apply(x, residual, bn.weight, bn.bias, rm, rv, batch_stats, bn.momentum, bn.eps, act, slope)
+    # num_batches_tracked is incremented by the statistics kernel (no extra launch)
+    nbt = bn.num_batches_tracked if update else None
+    return _BNAct.apply(x, residual, bn.weight, bn.bias, rm, rv, nbt, batch_stats, bn.momentum, bn.eps, act, slope)
 
 
 def _act_of(m):

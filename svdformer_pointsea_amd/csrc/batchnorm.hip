@@ -192,7 +192,8 @@ __global__ __launch_bounds__(512) void bn_final_kernel(const float *__restrict__
                                                        float *__restrict__ rvar, float momentum, float eps,
                                                        float *__restrict__ mean_io, float *__restrict__ invstd_io,
                                                        float *__restrict__ dgamma, float *__restrict__ dbeta,
-                                                       int eval, float *__restrict__ coef) {
+                                                       int eval, float *__restrict__ coef,
+                                                       long long *__restrict__ nbt) {
   __shared__ double red[2][16][33];
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -238,6 +239,7 @@ __global__ __launch_bounds__(512) void bn_final_kernel(const float *__restrict__
       const double unbiased = rows > 1 ? var * n / (n - 1.0) : var;
       rvar[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)rvar[c]);
     }
+    if (nbt && c == 0) nbt[0] += 1;  // module.num_batches_tracked (no separate add launch)
     const double sc = g * (double)invstd;
     coef[c] = (float)sc;
     coef[C + c] = (float)((beta ? (double)beta[c] : 0.0) - (double)(float)mean * sc);
@@ -390,7 +392,8 @@ extern "C" int pcops_batchnorm_fwd(const void *x, int dtype, const void *res, in
                                    const float *gamma, const float *beta, float *running_mean, float *running_var,
                                    float momentum, float eps, int batch_stats, int act, float slope, void *y,
                                    float *save_mean, float *save_invstd, void *workspace,
-                                   unsigned long long workspace_bytes, pcops_stream_t stream) {
+                                   unsigned long long workspace_bytes, long long *num_batches_tracked,
+                                   pcops_stream_t stream) {
   if (rows < 0 || C <= 0 || (dtype != 0 && dtype != 1) || act < 0 || act > 2) return PCOPS_ERR_INVALID;
   if (res && res_dtype != 0 && res_dtype != 1) return PCOPS_ERR_INVALID;
   if (rows == 0) return PCOPS_OK;
@@ -410,12 +413,12 @@ extern "C" int pcops_batchnorm_fwd(const void *x, int dtype, const void *res, in
       launch_partial<0>(0, x, nullptr, nullptr, nullptr, rows, C, 0.f, part, chunks, rpc, s);
       hipLaunchKernelGGL((bn_final_kernel<0, 0>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
                          gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, nullptr,
-                         nullptr, 0, coef);
+                         nullptr, 0, coef, running_mean ? num_batches_tracked : nullptr);
     } else {
       launch_partial<1>(0, x, nullptr, nullptr, nullptr, rows, C, 0.f, part, chunks, rpc, s);
       hipLaunchKernelGGL((bn_final_kernel<0, 1>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
                          gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, nullptr,
-                         nullptr, 0, coef);
+                         nullptr, 0, coef, running_mean ? num_batches_tracked : nullptr);
     }
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, running_mean,
@@ -462,12 +465,12 @@ extern "C" int pcops_batchnorm_bwd(const void *dy, const void *y, const void *x,
     launch_partial<0>(mode, x, dy, y, save_mean, rows, C, slope, part, chunks, rpc, s);
     hipLaunchKernelGGL((bn_final_kernel<1, 0>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
                        gamma, nullptr, nullptr, nullptr, 0.f, 0.f, (float *)save_mean, (float *)save_invstd, dgamma,
-                       dbeta, batch_stats ? 0 : 1, coef);
+                       dbeta, batch_stats ? 0 : 1, coef, nullptr);
   } else {
     launch_partial<1>(mode, x, dy, y, save_mean, rows, C, slope, part, chunks, rpc, s);
     hipLaunchKernelGGL((bn_final_kernel<1, 1>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
                        gamma, nullptr, nullptr, nullptr, 0.f, 0.f, (float *)save_mean, (float *)save_invstd, dgamma,
-                       dbeta, batch_stats ? 0 : 1, coef);
+                       dbeta, batch_stats ? 0 : 1, coef, nullptr);
   }
   const unsigned n8 = (unsigned)(rows * C / 8);
   const bool r = dres != nullptr;

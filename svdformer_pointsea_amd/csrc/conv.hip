@@ -17,8 +17,8 @@
 //   K = pixels: both operands are read with ds_read_b64_tr_b16 (4 pixels x 16
 //   channels per 16-lane group, delivered channel-major) from LDS images of the
 //   dy tile and the haloed x tile; one A fragment serves the 9 taps.  Each block
-//   loops over tiles, keeps its partial dW in registers and writes it once; a
-//   second kernel sums the block partials in a fixed order (deterministic).
+//   loops over tiles (prefetching the next one), keeps its partial dW in registers and
+//   writes it once; two small kernels sum the block partials in a fixed order (deterministic).
 #include "common.h"
 
 namespace {
@@ -30,39 +30,53 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTH = 4;        // output rows per tile (one per wave)
 constexpr int kTW = 64;       // output columns per tile
-constexpr int kLW = kTW + 2;  // haloed input tile columns
+[[maybe_unused]] constexpr int kLW = kTW + 2;  // haloed input tile columns (weight gradient)
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8 &a, const bf16x8 &b, const f32x4 &c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// stage the haloed input tile rows h0-1 .. h0+kTH, cols w0-1 .. w0+kTW of image n
-// (zeros outside the image) as [row][col][C] bf16
-template <int C>
-__device__ __forceinline__ void stage_halo(__bf16 *tile, const __bf16 *__restrict__ x, int n, int h0, int w0, int H,
-                                           int W) {
-  constexpr int VPP = C / 8;
-  for (int i = threadIdx.x; i < (kTH + 2) * kLW * VPP; i += 256) {
-    const int v = i % VPP, pc = i / VPP, c = pc % kLW, r = pc / kLW;
-    const int hh = h0 - 1 + r, ww = w0 - 1 + c;
-    bf16x8 val = {};
-    if (hh >= 0 && hh < H && ww >= 0 && ww < W)
-      val = *reinterpret_cast<const bf16x8 *>(x + (((long long)n * H + hh) * W + ww) * C + 8 * v);
-    *reinterpret_cast<bf16x8 *>(tile + (r * kLW + c) * C + 8 * v) = val;
+// Tile staging, global -> registers -> LDS, split in two halves so a block can
+// issue every load of a tile before its first LDS write (one memory latency per
+// tile instead of one per 16-B vector) and can prefetch the next tile while it
+// computes.  A rectangle of R rows x L columns x C channels starting at (hb, wb)
+// of image n is held as [row][col][C] bf16; outside the image reads as zero.
+template <int C, int R, int L>
+struct Stage {
+  static constexpr int VPP = C / 8, TOT = R * L * VPP, PER = (TOT + 255) / 256;
+  bf16x8 v[PER];
+  __device__ __forceinline__ void load(const __bf16 *__restrict__ x, int n, int hb, int wb, int H, int W) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int vv = i % VPP, pc = i / VPP, c = pc % L, r = pc / L;
+      const int hh = hb + r, ww = wb + c;
+      v[j] = bf16x8{};
+      if (i < TOT && hh >= 0 && hh < H && ww >= 0 && ww < W)
+        v[j] = *reinterpret_cast<const bf16x8 *>(x + (((long long)n * H + hh) * W + ww) * C + 8 * vv);
+    }
   }
-}
+  __device__ __forceinline__ void store(__bf16 *tile) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      if (i < TOT) *reinterpret_cast<bf16x8 *>(tile + 8 * i) = v[j];
+    }
+  }
+};
 
 // ---------------------------------------------------------------- forward / dgrad
-template <int CI, int CO>
+template <int CI, int CO, int TW>
 __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(const __bf16 *__restrict__ x,
                                                           const __bf16 *__restrict__ w, __bf16 *__restrict__ y,
                                                           int H, int W) {
   constexpr int KC = (9 * CI + 31) / 32;  // K chunks of 32 over (tap, ci); the tail has zero weights
   constexpr int MT = CO / 16;
-  __shared__ __attribute__((aligned(16))) __bf16 tile[(kTH + 2) * kLW * CI];
-  const int n = blockIdx.z, h0 = blockIdx.y * kTH, w0 = blockIdx.x * kTW;
+  constexpr int LW = TW + 2;
+  __shared__ __attribute__((aligned(16))) __bf16 tile[(kTH + 2) * LW * CI];
+  const int n = blockIdx.z, h0 = blockIdx.y * kTH, w0 = blockIdx.x * TW;
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l >> 4, i16 = l & 15;
-  stage_halo<CI>(tile, x, n, h0, w0, H, W);
+  // weight fragments and the input tile loads issued together (one memory latency)
   bf16x8 a[MT][KC];
 #pragma unroll
   for (int c = 0; c < KC; ++c) {
@@ -71,10 +85,15 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(const __bf16 *__restri
     for (int mt = 0; mt < MT; ++mt)
       a[mt][c] = tap < 9 ? *reinterpret_cast<const bf16x8 *>(w + ((16 * mt + i16) * 9 + tap) * CI + ci0) : bf16x8{};
   }
+  {
+    Stage<CI, kTH + 2, LW> st;
+    st.load(x, n, h0 - 1, w0 - 1, H, W);
+    st.store(tile);
+  }
   __syncthreads();
   const int orow = h0 + wv;
 #pragma unroll
-  for (int nt = 0; nt < kTW / 16; ++nt) {
+  for (int nt = 0; nt < TW / 16; ++nt) {
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -84,7 +103,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(const __bf16 *__restri
       const int k0 = 32 * c + 8 * g;
       const int tap = k0 / CI < 9 ? k0 / CI : 8;  // K tail: finite data against zero weights
       const int ci0 = k0 % CI, dh = tap / 3, dw = tap % 3;
-      const bf16x8 b = *reinterpret_cast<const bf16x8 *>(tile + ((wv + dh) * kLW + pc + dw) * CI + ci0);
+      const bf16x8 b = *reinterpret_cast<const bf16x8 *>(tile + ((wv + dh) * LW + pc + dw) * CI + ci0);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(a[mt][c], b, acc[mt]);
     }
@@ -128,22 +147,22 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(const __bf16 *__rest
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[t][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+  Stage<CI, kTH + 2, kLW> sx;
+  Stage<CO, kTH, kTW> sg;
+  auto fetch = [&](long long t) {
     const int bx = (int)(t % tw);
     const long long r = t / tw;
     const int by = (int)(r % th), n = (int)(r / th);
-    const int h0 = by * kTH, w0 = bx * kTW;
-    __syncthreads();  // the previous tile's reads are done
-    stage_halo<CI>(xt, x, n, h0, w0, H, W);
-    constexpr int VPO = CO / 8;
-    for (int i = threadIdx.x; i < kTH * kTW * VPO; i += 256) {
-      const int v = i % VPO, pc = i / VPO, c = pc % kTW, rr = pc / kTW;
-      const int hh = h0 + rr, ww = w0 + c;
-      bf16x8 val = {};
-      if (hh < H && ww < W) val = *reinterpret_cast<const bf16x8 *>(dy + (((long long)n * H + hh) * W + ww) * CO + 8 * v);
-      *reinterpret_cast<bf16x8 *>(gt + (rr * kTW + c) * CO + 8 * v) = val;
-    }
+    sx.load(x, n, by * kTH - 1, bx * kTW - 1, H, W);
+    sg.load(dy, n, by * kTH, bx * kTW, H, W);
+  };
+  if (blockIdx.x < tiles) fetch(blockIdx.x);
+  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's LDS reads are done
+    sx.store(xt);
+    sg.store(gt);
     __syncthreads();
+    if (t + gridDim.x < tiles) fetch(t + gridDim.x);  // next tile's loads fly during this tile's MFMAs
 #pragma unroll
     for (int kc = 0; kc < kTW / 32; ++kc) {
       // pixels 32kc + 8g + (0..3 | 4..7) of row wv; lane 4q+p addresses row q, channels 4p..4p+3
@@ -201,25 +220,34 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(const __bf16 *__rest
 #endif
 }
 
-// dw = sum over blocks of part[b][co][tap][ci], written in the weight's memory
-// order -- OIHW [co][ci][kh][kw] or channels_last OHWI [co][kh][kw][ci] -- as fp32
-// or bf16 (the dtype of the weight it is the gradient of)
-__global__ __launch_bounds__(256) void conv3x3_wgrad_final_kernel(const float *__restrict__ part, int blocks, int CO,
-                                                                  int CI, void *__restrict__ out, int odt,
-                                                                  int ohwi) {
+// dw = sum over blocks of part[b][co][tap][ci] in two fixed-order stages (a
+// single pass had each thread walk all block rows: ~1 us of latency per 8 rows):
+//   reduce1: part2[s][e] = sum_{b = s, s + kSplit, ...} part[b][e]       grid (E/256, kSplit)
+//   reduce2: dw = sum_s part2[s][e], written in the weight's memory order -- OIHW
+//            [co][ci][kh][kw] or channels_last OHWI [co][kh][kw][ci] -- as fp32 or bf16
+constexpr int kSplit = 32;
+
+__global__ __launch_bounds__(256) void conv3x3_wgrad_reduce1_kernel(const float *__restrict__ part, int blocks, int E,
+                                                                    float *__restrict__ part2) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= E) return;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int b = blockIdx.y;
+  for (; b + 7 * kSplit < blocks; b += 8 * kSplit)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += part[(long long)(b + j * kSplit) * E + e];
+  for (; b < blocks; b += kSplit) acc[0] += part[(long long)b * E + e];
+  part2[(long long)blockIdx.y * E + e] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+__global__ __launch_bounds__(256) void conv3x3_wgrad_reduce2_kernel(const float *__restrict__ part2, int CO, int CI,
+                                                                    void *__restrict__ out, int odt, int ohwi) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   const int E = 9 * CO * CI;
   if (e >= E) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int b = 0;
-  for (; b + 3 < blocks; b += 4) {
-    s0 += part[(long long)b * E + e];
-    s1 += part[(long long)(b + 1) * E + e];
-    s2 += part[(long long)(b + 2) * E + e];
-    s3 += part[(long long)(b + 3) * E + e];
-  }
-  for (; b < blocks; ++b) s0 += part[(long long)b * E + e];
-  const float v = (s0 + s1) + (s2 + s3);
+  float v = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < kSplit; ++s2) v += part2[(long long)s2 * E + e];
   const int co = e / (9 * CI), rem = e - co * 9 * CI, tap = rem / CI, ci = rem - tap * CI;
   const int o = ohwi ? e : (co * CI + ci) * 9 + tap;
   if (odt == 0)
@@ -240,21 +268,27 @@ extern "C" int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int
   if (N == 0 || H == 0 || W == 0) return PCOPS_OK;
   if (!conv_ok(N, H, W, C)) return PCOPS_ERR_UNSUPPORTED;
   if (!x || !w || !y) return PCOPS_ERR_INVALID;
-  const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, N);
   hipStream_t s = (hipStream_t)stream;
-  if (C == 16)
-    hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16>), grid, dim3(256), 0, s, (const __bf16 *)x, (const __bf16 *)w,
-                       (__bf16 *)y, H, W);
-  else
-    hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32>), grid, dim3(256), 0, s, (const __bf16 *)x, (const __bf16 *)w,
-                       (__bf16 *)y, H, W);
+  // 112-column tiles where they divide W exactly (the 224 / 112 images): no masked N-tiles
+  const bool wide = W % 112 == 0;
+  const int TW = wide ? 112 : 64;
+  const dim3 grid((W + TW - 1) / TW, (H + kTH - 1) / kTH, N);
+  const __bf16 *xp = (const __bf16 *)x, *wp = (const __bf16 *)w;
+  __bf16 *yp = (__bf16 *)y;
+  if (C == 16) {
+    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
+  } else {
+    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
+  }
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
 
 extern "C" unsigned long long pcops_conv3x3_wgrad_workspace_bytes(int C) {
   if (C != 16 && C != 32) return 0;
-  return (unsigned long long)wgrad_blocks(C) * 9 * C * C * sizeof(float);
+  return (unsigned long long)(wgrad_blocks(C) + kSplit) * 9 * C * C * sizeof(float);
 }
 
 extern "C" int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, int W, int C, void *dw, int dw_dtype,
@@ -277,7 +311,10 @@ extern "C" int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, 
   else
     hipLaunchKernelGGL((conv3x3_wgrad_kernel<32, 32>), dim3(G), dim3(256), 0, s, (const __bf16 *)x,
                        (const __bf16 *)dy, N, H, W, part);
-  hipLaunchKernelGGL(conv3x3_wgrad_final_kernel, dim3((9 * C * C + 255) / 256), dim3(256), 0, s, part, G, C, C, dw, dw_dtype,
+  float *part2 = part + (long long)G * 9 * C * C;
+  const int E = 9 * C * C;
+  hipLaunchKernelGGL(conv3x3_wgrad_reduce1_kernel, dim3((E + 255) / 256, kSplit), dim3(256), 0, s, part, G, E, part2);
+  hipLaunchKernelGGL(conv3x3_wgrad_reduce2_kernel, dim3((E + 255) / 256), dim3(256), 0, s, part2, C, C, dw, dw_dtype,
                      dw_ohwi);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
