@@ -293,6 +293,16 @@ unsigned long long pcops_conv3x3_wgrad_workspace_bytes(int C);
 int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, int W, int C, void *dw, int dw_dtype,
                         int dw_ohwi, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 
+/* The single-channel stem of the same encoder, nn.Conv2d(1, 16, 3, padding=1, bias=False)
+ * (models/SVDFormer.py:139-140): x (N, H, W) fp32 (rounded to bf16 as autocast's conv does),
+ * w (16, 1, 3, 3) fp32, y (N, H, W, 16) bf16 channels_last; fp32 accumulation.
+ * pcops_conv3x3_c1_wgrad: dw (16, 1, 3, 3) as fp32 (dw_dtype 0) or bf16 (1).
+ *   workspace: pcops_conv3x3_c1_wgrad_workspace_bytes(). */
+int pcops_conv3x3_c1_fwd(const float *x, const float *w, int N, int H, int W, void *y, pcops_stream_t stream);
+unsigned long long pcops_conv3x3_c1_wgrad_workspace_bytes(void);
+int pcops_conv3x3_c1_wgrad(const float *x, const void *dy, int N, int H, int W, void *dw, int dw_dtype, void *workspace,
+                           unsigned long long workspace_bytes, pcops_stream_t stream);
+
 /* ---------------- PCSA spectral gating (models/model_utils.py:358-430) ----------------
  * Per patch p (= b*S + s) of K neighbours x C channels stored [p][k][c] (the
  * channels_last memory order of the (B, C, S, K) conv output):

@@ -69,6 +69,9 @@ _SIGS = {
     "pcops_conv3x3_fwd": (I, [P, P, I, I, I, I, P, P]),
     "pcops_conv3x3_wgrad_workspace_bytes": (ULL, [I]),
     "pcops_conv3x3_wgrad": (I, [P, P, I, I, I, I, P, I, I, P, ULL, P]),
+    "pcops_conv3x3_c1_fwd": (I, [P, P, I, I, I, P, P]),
+    "pcops_conv3x3_c1_wgrad_workspace_bytes": (ULL, []),
+    "pcops_conv3x3_c1_wgrad": (I, [P, P, I, I, I, P, I, P, ULL, P]),
     "pcops_pcsa_forward": (I, [P, I, P, I, P, I, I, I, P, P]),
     "pcops_pcsa_backward": (I, [P, I, P, I, P, I, P, I, I, I, P, P, P]),
     "pcops_points2depth_workspace_bytes": (ULL, [I, I, I, I]),

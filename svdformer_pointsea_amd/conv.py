@@ -1,5 +1,6 @@
 """3x3 / stride 1 / pad 1 / bias-free nn.Conv2d on channels_last bf16 activations
-through libpcops (pcops_conv3x3_fwd / _wgrad, csrc/conv.hip): the ResNet
+through libpcops (pcops_conv3x3_fwd / _wgrad, csrc/conv.hip) -- and the
+single-channel stem conv on the fp32 depth images (pcops_conv3x3_c1_*): the ResNet
 BasicBlock convs of SVDFormer's image encoder (models/resnet.py:36-70 via
 models/SVDFormer.py:139-146; C = 16 at 224x224 and 32 at 112x112 for the 96
 depth images of a PCN batch), where MIOpen's NHWC kernels ran 2.5-6x below
@@ -57,6 +58,46 @@ class _Conv3x3(torch.autograd.Function):
         return gx, gw
 
 
+class _Conv3x3C1(torch.autograd.Function):
+    """The single-channel stem (nn.Conv2d(1, 16, 3, padding=1, bias=False) on fp32 depth
+    images under bf16 autocast): pcops_conv3x3_c1_fwd / _wgrad; the image gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        N, _, H, W = x.shape
+        y = torch.empty((N, 16, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        with torch.cuda.device(x.device):
+            call("conv3x3_c1_fwd", lib().pcops_conv3x3_c1_fwd, ptr(x), ptr(w.float().contiguous()), N, H, W, ptr(y),
+                 stream_of(x))
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        N, _, H, W = x.shape
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gy = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            gw = torch.empty_like(w)   # Cin = 1: OIHW and OHWI are the same order
+            with torch.cuda.device(x.device):
+                nbytes = lib().pcops_conv3x3_c1_wgrad_workspace_bytes()
+                ws = Workspace.get(x.device, nbytes)
+                call("conv3x3_c1_wgrad", lib().pcops_conv3x3_c1_wgrad, ptr(x), ptr(gy), N, H, W, ptr(gw),
+                     0 if w.dtype == torch.float32 else 1, ptr(ws), nbytes, stream_of(x))
+        return None, gw
+
+
+def stem_eligible(x, conv):
+    return (ENABLED and isinstance(conv, nn.Conv2d) and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
+            and not x.requires_grad and x.shape[1] == 1 and x.is_contiguous()
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and conv.in_channels == 1 and conv.out_channels == 16 and conv.kernel_size == (3, 3)
+            and conv.stride == (1, 1) and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.bias is None and conv.padding_mode == "zeros"
+            and conv.weight.dtype in (torch.float32, torch.bfloat16) and conv.weight.is_contiguous())
+
+
 def eligible(x, conv):
     if not (ENABLED and isinstance(conv, nn.Conv2d) and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16):
         return False
@@ -74,4 +115,6 @@ def conv3x3(x, conv, weight=None):
     w = conv.weight if weight is None else weight
     if eligible(x, conv) and w.dtype in (torch.float32, torch.bfloat16):
         return _Conv3x3.apply(x, w)
+    if stem_eligible(x, conv):
+        return _Conv3x3C1.apply(x, w)
     return conv(x)

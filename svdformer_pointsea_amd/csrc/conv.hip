@@ -260,6 +260,122 @@ int wgrad_blocks(int C) { return C <= 16 ? 1024 : 512; }
 
 bool conv_ok(int N, int H, int W, int C) { return N > 0 && H > 0 && W > 0 && (C == 16 || C == 32); }
 
+// ---------------------------------------------------------------- single-channel stem
+// SVDFormer's image stem nn.Conv2d(1, 16, 3, padding=1, bias=False) on the (3B, 1, 224, 224)
+// fp32 depth images (models/SVDFormer.py:139-140): K = 9 is too short for MFMA, so VALU.
+// The input is rounded to bf16 as autocast's conv would; products accumulate in fp32.
+// fwd: one thread per output pixel, the 3 x 3 window from an LDS image of the block's
+// (4 + 2) x (64 + 2) input rows, the 16 x 9 weights uniform (scalar loads), 16 bf16 out.
+constexpr int kC1Out = 16;
+
+__device__ __forceinline__ float bf16r(float v) { return (float)(__bf16)v; }
+
+__global__ __launch_bounds__(256) void conv3x3_c1_fwd_kernel(const float *__restrict__ x,
+                                                             const float *__restrict__ w, __bf16 *__restrict__ y,
+                                                             int H, int W) {
+  __shared__ float tile[(kTH + 2) * (kTW + 2)];
+  const int n = blockIdx.z, h0 = blockIdx.y * kTH, w0 = blockIdx.x * kTW;
+  for (int i = threadIdx.x; i < (kTH + 2) * (kTW + 2); i += 256) {
+    const int r = i / (kTW + 2), c = i - r * (kTW + 2);
+    const int hh = h0 - 1 + r, ww = w0 - 1 + c;
+    tile[i] = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? bf16r(x[((long long)n * H + hh) * W + ww]) : 0.f;
+  }
+  __syncthreads();
+  const int r = threadIdx.x >> 6, c = threadIdx.x & 63;
+  const int oh = h0 + r, ow = w0 + c;
+  if (oh >= H || ow >= W) return;
+  float v[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) v[t] = tile[(r + t / 3) * (kTW + 2) + c + t % 3];
+  bf16x8 o[2];
+#pragma unroll
+  for (int co = 0; co < kC1Out; ++co) {
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc = __builtin_fmaf(v[t], bf16r(w[co * 9 + t]), acc);
+    o[co >> 3][co & 7] = (__bf16)acc;
+  }
+  bf16x8 *yp = reinterpret_cast<bf16x8 *>(y + (((long long)n * H + oh) * W + ow) * kC1Out);
+  yp[0] = o[0];
+  yp[1] = o[1];
+}
+
+// wgrad: dW[co][tap] = sum_p dy[p][co] * x[p + off(tap)]; G blocks stride over the
+// 4 x 64 output tiles, each thread accumulating its pixels' 144 products in registers;
+// wave (DPP) + LDS block reduction, one partial row per block (summed by the reduce
+// kernels below, in a fixed order)
+__global__ __launch_bounds__(256) void conv3x3_c1_wgrad_kernel(const float *__restrict__ x,
+                                                               const __bf16 *__restrict__ dy, int N, int H, int W,
+                                                               float *__restrict__ part) {
+  __shared__ float tile[(kTH + 2) * (kTW + 2)];
+  __shared__ float red[4][kC1Out * 9];
+  const int tw = (W + kTW - 1) / kTW, th = (H + kTH - 1) / kTH;
+  const long long tiles = (long long)N * th * tw;
+  const int r = threadIdx.x >> 6, c = threadIdx.x & 63;
+  float acc[kC1Out * 9];
+#pragma unroll
+  for (int i = 0; i < kC1Out * 9; ++i) acc[i] = 0.f;
+  // registers holding the NEXT tile (its loads fly while this tile's products run)
+  constexpr int XPER = ((kTH + 2) * (kTW + 2) + 255) / 256;
+  float xv[XPER];
+  bf16x8 g0 = {}, g1 = {};
+  auto fetch = [&](long long t) {
+    const int bx = (int)(t % tw);
+    const long long rr = t / tw;
+    const int by = (int)(rr % th), n = (int)(rr / th);
+    const int h0 = by * kTH, w0 = bx * kTW;
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int ir = i / (kTW + 2), ic = i - ir * (kTW + 2);
+      const int hh = h0 - 1 + ir, ww = w0 - 1 + ic;
+      xv[j] = (i < (kTH + 2) * (kTW + 2) && hh >= 0 && hh < H && ww >= 0 && ww < W)
+                  ? x[((long long)n * H + hh) * W + ww] : 0.f;
+    }
+    const int oh = h0 + r, ow = w0 + c;
+    g0 = bf16x8{};
+    g1 = bf16x8{};
+    if (oh < H && ow < W) {
+      const bf16x8 *gp = reinterpret_cast<const bf16x8 *>(dy + (((long long)n * H + oh) * W + ow) * kC1Out);
+      g0 = gp[0];
+      g1 = gp[1];
+    }
+  };
+  if (blockIdx.x < tiles) fetch(blockIdx.x);
+  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's LDS reads are done
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      if (i < (kTH + 2) * (kTW + 2)) tile[i] = bf16r(xv[j]);
+    }
+    const bf16x8 c0 = g0, c1 = g1;
+    __syncthreads();
+    if (t + gridDim.x < tiles) fetch(t + gridDim.x);
+    float v[9];
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) v[tp] = tile[(r + tp / 3) * (kTW + 2) + c + tp % 3];
+#pragma unroll
+    for (int co = 0; co < kC1Out; ++co) {
+      const float g = (float)(co < 8 ? c0[co] : c1[co - 8]);
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) acc[co * 9 + tp] = __builtin_fmaf(g, v[tp], acc[co * 9 + tp]);
+    }
+  }
+  // wave sums (xor shuffles), then the four waves through LDS in a fixed order
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < kC1Out * 9; ++i) {
+    float v = acc[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[wv][i] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kC1Out * 9; i += 256)
+    part[(long long)blockIdx.x * kC1Out * 9 + i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+}
+
 }  // namespace
 
 extern "C" int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int W, int C, void *y,
@@ -316,6 +432,45 @@ extern "C" int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, 
   hipLaunchKernelGGL(conv3x3_wgrad_reduce1_kernel, dim3((E + 255) / 256, kSplit), dim3(256), 0, s, part, G, E, part2);
   hipLaunchKernelGGL(conv3x3_wgrad_reduce2_kernel, dim3((E + 255) / 256), dim3(256), 0, s, part2, C, C, dw, dw_dtype,
                      dw_ohwi);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_conv3x3_c1_fwd(const float *x, const float *w, int N, int H, int W, void *y,
+                                    pcops_stream_t stream) {
+  if (N < 0 || H < 0 || W < 0) return PCOPS_ERR_INVALID;
+  if (N == 0 || H == 0 || W == 0) return PCOPS_OK;
+  if (!x || !w || !y) return PCOPS_ERR_INVALID;
+  const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, N);
+  hipLaunchKernelGGL(conv3x3_c1_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, w, (__bf16 *)y, H, W);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+constexpr int kC1Blocks = 1024;
+
+extern "C" unsigned long long pcops_conv3x3_c1_wgrad_workspace_bytes(void) {
+  return (unsigned long long)(kC1Blocks + kSplit) * kC1Out * 9 * sizeof(float);
+}
+
+extern "C" int pcops_conv3x3_c1_wgrad(const float *x, const void *dy, int N, int H, int W, void *dw, int dw_dtype,
+                                      void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (N < 0 || H < 0 || W < 0 || !dw || (dw_dtype != 0 && dw_dtype != 1)) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 0 || H == 0 || W == 0) {
+    if (hipMemsetAsync(dw, 0, (dw_dtype == 0 ? 4 : 2) * kC1Out * 9, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!x || !dy) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_conv3x3_c1_wgrad_workspace_bytes()) return PCOPS_ERR_WORKSPACE;
+  float *part = (float *)workspace, *part2 = part + (long long)kC1Blocks * kC1Out * 9;
+  const int E = kC1Out * 9;
+  hipLaunchKernelGGL(conv3x3_c1_wgrad_kernel, dim3(kC1Blocks), dim3(256), 0, s, x, (const __bf16 *)dy, N, H, W, part);
+  hipLaunchKernelGGL(conv3x3_wgrad_reduce1_kernel, dim3((E + 255) / 256, kSplit), dim3(256), 0, s, part, kC1Blocks,
+                     E, part2);
+  // CI = 1: OIHW [co][0][kh][kw] and OHWI [co][kh][kw][0] are the same order
+  hipLaunchKernelGGL(conv3x3_wgrad_reduce2_kernel, dim3((E + 255) / 256), dim3(256), 0, s, part2, kC1Out, 1, dw,
+                     dw_dtype, 1);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

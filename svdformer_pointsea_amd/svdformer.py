@@ -520,7 +520,9 @@ class SVFNet(nn.Module):
     def forward(self, points, depth):
         batch_size, _, N = points.size()
         depth = depth.contiguous(memory_format=torch.channels_last)
-        f_v = run_sequential(self.img_feature_extractor, depth).view(batch_size, 3, -1).transpose(1, 2).contiguous()
+        # stem conv (1 -> 16) on libpcops under bf16 autocast, each BN + ReLU fused
+        f_v = run_sequential(self.img_feature_extractor, depth, conv3x3).view(batch_size, 3, -1).transpose(1, 2)
+        f_v = f_v.contiguous()
         f_p = self.point_feature_extractor(points)
         view_point = self.view_point.expand(batch_size, 3, 3)
         view_feature = self.posmlp(view_point).permute(2, 0, 1)

@@ -113,3 +113,39 @@ def test_basic_block_conv_vs_miopen(dev, monkeypatch, C, HW):
         # sum(dy * mask)): ReLU flips on either path move them by a few %, so a looser margin
         slack = (1.25, 2e-3) if name in ("y", "dx") else (1.5, 2e-2)
         assert ea <= slack[0] * eb + slack[1], f"{name}: libpcops conv rel err {ea:.3g} vs MIOpen {eb:.3g}"
+
+
+@pytest.mark.parametrize("shape", [(3, 1, 224, 224), (2, 1, 37, 70)])
+@pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
+def test_stem_conv_vs_float64(dev, shape, wdt):
+    """The 1 -> 16 stem: x rounded to bf16 and bf16 weights (autocast's operands), fp32 sums."""
+    g = torch.Generator().manual_seed(shape[2])
+    x = torch.rand(shape, generator=g) * 2.0
+    w = (torch.randn(16, 1, 3, 3, generator=g) / 3).to(wdt)
+    dy = torch.randn(shape[0], 16, shape[2], shape[3], generator=g).to(torch.bfloat16)
+    wg = w.to(dev).requires_grad_(True)
+    y = CV._Conv3x3C1.apply(x.to(dev), wg)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(dy.to(dev).contiguous(memory_format=torch.channels_last))
+    assert wg.grad.dtype == wdt
+    x64 = x.to(torch.bfloat16).double()
+    w64 = w.to(torch.bfloat16).double().requires_grad_(True)
+    y64 = F.conv2d(x64, w64, padding=1)
+    y64.backward(dy.double())
+    torch.testing.assert_close(y.double().cpu(), y64.detach(), atol=2 ** -8 * y64.abs().mean().item(), rtol=2 ** -8)
+    gw = wg.grad.double().cpu()
+    if wdt == torch.float32:
+        assert ((gw - w64.grad).norm() / w64.grad.norm()) < 1e-5
+    else:
+        torch.testing.assert_close(gw, w64.grad, atol=2 ** -8 * w64.grad.abs().mean().item(), rtol=2 ** -8)
+
+
+def test_stem_eligibility(dev):
+    conv = nn.Conv2d(1, 16, 3, padding=1, bias=False).to(dev)
+    x = torch.rand(2, 1, 16, 16, device=dev)
+    assert not CV.stem_eligible(x, conv)          # needs bf16 autocast (torch would compute in fp32)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert CV.stem_eligible(x, conv)
+        assert not CV.stem_eligible(x, nn.Conv2d(1, 16, 3, padding=1, bias=True).to(dev))
+        y = CV.conv3x3(x, conv)
+    assert y.dtype == torch.bfloat16
