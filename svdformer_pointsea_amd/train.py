@@ -79,6 +79,12 @@ class FlatParams:
         self.shadow = {}
         self._order = []   # bf16-eligible shadows in bucket order
         self._offset = {}  # parameter name -> offset in the flat buffers
+        # with bf16 shadows (collect() required anyway) autograd also owns the fp32
+        # parameters' gradients: a preset .grad view made AccumulateGrad launch one add
+        # kernel per fp32 parameter per step (~90 LayerNorm / BatchNorm tensors, 0.45 ms
+        # per PCN step); collect() gathers them with one batched copy instead
+        self._own32 = bool(low) and _GRADS == "cat"
+        self._order32 = []  # (parameter, its bucket view) of the trainable fp32 region
         off = 0
         with torch.no_grad():
             for name, p in named:
@@ -88,6 +94,8 @@ class FlatParams:
                 view.copy_(p.data)
                 p.data = view
                 p.grad = self.grad[off:off + n].as_strided(p.shape, p.stride())
+                if self._own32 and name not in low and name not in frozen:
+                    self._order32.append((p, p.grad))
                 if name in low:
                     w = self.flat16[off:off + n].as_strided(p.shape, p.stride())
                     w.requires_grad_(True)
@@ -96,6 +104,8 @@ class FlatParams:
                     self.shadow[name] = w
                     self._order.append(w)
                 off += n
+        n32 = max((p.numel() for p, _ in self._order32), default=0)
+        self._zeros32 = torch.zeros(n32, dtype=torch.float32, device=device)
 
     def master(self):
         """The whole fp32 master buffer as ONE parameter whose .grad is the bucket.
@@ -111,7 +121,11 @@ class FlatParams:
         return p
 
     def zero_grad(self):
-        self.grad[self.n16:].zero_()   # grad[:n16] is overwritten by collect()
+        if self._own32:
+            for p, _ in self._order32:
+                p.grad = None          # grad[n16:n_train] is overwritten by collect()
+        else:
+            self.grad[self.n16:].zero_()   # grad[:n16] is overwritten by collect()
         if _GRADS == "preset":
             self.grad16.zero_()
             return
@@ -154,6 +168,20 @@ class FlatParams:
                              if g is None else self._physical(g, w))
             torch.cat(parts, out=self.grad16)
             self.grad[:self.n16].copy_(self.grad16)
+            self._collect32(self.n16, self.n_train, self._order32)
+
+    def _collect32(self, lo, hi, entries):
+        """bucket[lo:hi] <- the fp32 gradients autograd produced for `entries` (flat order),
+        zeros where none arrived; .grad points at the bucket again afterwards."""
+        if not self._own32 or not entries:
+            return
+        parts = []
+        for p, view in entries:
+            g = p.grad
+            parts.append(self._zeros32[:p.numel()] if g is None else self._physical(g, p))
+        torch.cat(parts, out=self.grad[lo:hi])
+        for p, view in entries:
+            p.grad = view
 
     def allreduce(self, world):
         """The data-parallel step's only collective: mean of the flat bucket."""
@@ -265,6 +293,9 @@ class BucketedAllReduce:
                                  if g is None else fp._physical(g, w))
                 torch.cat(parts, out=fp.grad16[lo:hi])
                 fp.grad[lo:hi].copy_(fp.grad16[lo:hi])
+            elif fp._own32:   # fp32 parameters: autograd-owned gradients into the bucket
+                view = {id(p): v for p, v in fp._order32}
+                fp._collect32(lo, hi, [(w, view[id(w)]) for o, n, w, _ in sorted(es, key=lambda e: e[0])])
             seg = fp.grad[lo:hi]
             self.dist.all_reduce(seg, group=self.group)
             seg.mul_(1.0 / self.world)
