@@ -244,6 +244,10 @@ int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, long long ro
  *   Replaces the bias-gradient reduction autograd runs for nn.Linear / 1x1 nn.Conv*d biases
  *   (torch's g.sum(0) behind F.linear's backward; models/model_utils.py Linear / Conv1d layers).
  *   workspace: pcops_colsum_workspace_bytes(rows, C). */
+/* pcops_sum_rows: out[i] = sum_{s < S} part[s][i] for a row-major (S, N) fp32 matrix, fixed order, rounded
+ *   once to out_dtype (0 fp32, 1 bf16); N % 4 == 0, 16-byte aligned.  The split-K weight gradient's
+ *   partial sum + cast (torch's part.sum(0).to(dtype) behind the blocks' Linear layers). */
+int pcops_sum_rows(const float *part, int S, long long N, void *out, int out_dtype, pcops_stream_t stream);
 unsigned long long pcops_colsum_workspace_bytes(long long rows, int C);
 int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype, void *workspace,
                  unsigned long long workspace_bytes, pcops_stream_t stream);

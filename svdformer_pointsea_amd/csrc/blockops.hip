@@ -529,6 +529,28 @@ __global__ __launch_bounds__(256) void gelu_bwd_partial_kernel(const void *__res
   }
 }
 
+// Split-K weight-gradient epilogue: out[i] = sum_{s < S} part[s][i] (fixed order),
+// rounded once to out's dtype -- torch ran part.sum(0) (a reduce kernel) and .to(bf16)
+// (a copy kernel) per Linear.  Four elements per thread (16-B loads per row).
+__global__ __launch_bounds__(256) void sum_rows_kernel(const float *__restrict__ part, int S, long long n4,
+                                                       long long N, void *__restrict__ out, int odt) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 acc = *reinterpret_cast<const float4 *>(part + 4 * i);
+  for (int r = 1; r < S; ++r) {
+    const float4 v = *reinterpret_cast<const float4 *>(part + (long long)r * N + 4 * i);
+    acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+  }
+  if (odt == 0) {
+    *reinterpret_cast<float4 *>(reinterpret_cast<float *>(out) + 4 * i) = acc;
+  } else {
+    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+    bf16x4_t o;
+    o[0] = (__bf16)acc.x, o[1] = (__bf16)acc.y, o[2] = (__bf16)acc.z, o[3] = (__bf16)acc.w;
+    *reinterpret_cast<bf16x4_t *>(reinterpret_cast<__bf16 *>(out) + 4 * i) = o;
+  }
+}
+
 int colsum_v(int C) {  // vector columns per wave: largest power of two <= 64 dividing C / 8
   const int nv = C / 8;
   int V = 64;
@@ -771,6 +793,18 @@ extern "C" int pcops_colsum(const void *g, int g_dtype, long long rows, int C, v
     hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, out, out_dtype, C,
                      nullptr, C, nullptr);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_sum_rows(const float *part, int S, long long N, void *out, int out_dtype, pcops_stream_t stream) {
+  if (S <= 0 || N < 0 || !dt_ok(out_dtype)) return PCOPS_ERR_INVALID;
+  if (N == 0) return PCOPS_OK;
+  if (N % 4) return PCOPS_ERR_UNSUPPORTED;
+  if (!part || !out) return PCOPS_ERR_INVALID;
+  const long long n4 = N / 4;
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, part, S,
+                     n4, N, out, out_dtype);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

@@ -333,6 +333,25 @@ def test_colsum_matches_float64(dev, rows, C, dtype):
     assert bool((err <= atol + 1e-4 * ref.abs()).all()), err.max()
 
 
+@pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("T,Cout,Cin", [(65536, 512, 512), (16384, 768, 256), (8192, 1024, 512)])
+def test_split_k_wgrad_matches_float64(dev, wdt, T, Cout, Cin):
+    """The blocks' split-K weight gradient (bmm partials + pcops_sum_rows: fixed-order sum,
+    one rounding) vs float64 g^T x: within fp32 accumulation error (+ one bf16 rounding)."""
+    from svdformer_pointsea_amd import attention
+
+    g = torch.Generator(device=dev).manual_seed(T + Cout)
+    g2 = torch.randn(T, Cout, device=dev, generator=g).to(torch.bfloat16)
+    x2 = torch.randn(T, Cin, device=dev, generator=g).to(torch.bfloat16)
+    out = attention._wgrad(g2, x2, wdt)
+    assert out.dtype == wdt and out.shape == (Cout, Cin)
+    assert torch.equal(out, attention._wgrad(g2, x2, wdt))      # deterministic
+    ref = (g2.double().t() @ x2.double()).cpu()
+    err = (out.double().cpu() - ref).abs()
+    tol = 1e-5 * T ** 0.5 + (2 ** -8 * ref.abs() if wdt == torch.bfloat16 else 1e-5 * ref.abs())
+    assert bool((err <= tol).all()), float(err.max())
+
+
 @pytest.mark.parametrize("hd", [64, 128])
 def test_core_bf16_growing_row_max(dev, hd):
     """Scores that grow along the keys at a per-row rate, so row maxima rise
