@@ -649,25 +649,42 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    timed_loss = loss_hist[-1].item()   # running loss through the last timed step
+    timing_nonfinite = False
     if use_graph and not args.no_kernel_timing:
         # ROCm torch refuses timing events inside a captured graph ("External
         # events are disallowed in rocm"), so the per-launch HIP events come
-        # from eager steps of the same work right after the timed replays.
+        # from eager steps of the same work right after the timed replays --
+        # on a side stream, like the warm-up
         _lib.KernelTimer.enable()
-        for _ in range(args.timing_steps):
-            eager_step()
+        tstream = torch.cuda.Stream()
+        tstream.wait_stream(torch.cuda.current_stream())
+        before = loss_acc.clone()
+        master_before = fp.flat.clone()
+        with torch.cuda.stream(tstream):
+            for _ in range(args.timing_steps):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(tstream)
         torch.cuda.synchronize()
+        # the timing steps only supply kernel durations: a non-finite loss there is reported,
+        # not fatal (the timed replays above are what `value` measures)
+        timing_nonfinite = math.isfinite(before.item()) and not math.isfinite(loss_acc.item())
+        if timing_nonfinite:
+            progress("WARNING: non-finite loss in the eager kernel-timing steps after the timed replays; "
+                     "master weights restored for the configs[1] leg")
+            fp.flat.copy_(master_before)
+        del master_before
     spans = _lib.KernelTimer.spans or {}
     _lib.KernelTimer.disable()
     if use_dist:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    if not math.isfinite(loss_acc.item()):
+    if not math.isfinite(timed_loss):
         # where it started: the first non-finite running loss (0 = warm-up), and which
         # flat buffers / parameters carry non-finite values now
         hist = torch.stack(loss_hist).cpu()
-        bad = [i for i, v in enumerate(hist.tolist()) if not math.isfinite(v)]
+        bad = [i for i, v in enumerate(hist.tolist()) if not math.isfinite(v)] or [len(hist)]
         names = [n for n, q in model.named_parameters()
                  if not torch.isfinite(q.detach()).all() or (q.grad is not None and not torch.isfinite(q.grad).all())]
         progress(f"non-finite running loss from snapshot {bad[0]} of {len(hist)} (0 = after warm-up); "
@@ -694,6 +711,7 @@ def main():
             "ms_per_step": elapsed * 1e3 / args.steps,
             "host_issue_ms_per_step": host * 1e3 / args.steps,
             "execution": "hip_graph" if use_graph else "eager",
+            "kernel_timing_nonfinite": timing_nonfinite,
             "grad_sync": ("none (single GPU)" if not use_dist else
                           f"bucketed all-reduce from backward hooks ({len(sync[0].buckets)} buckets of "
                           f"<= {args.bucket_mb:g} MB){' inside the captured graph' if use_graph else ''}"

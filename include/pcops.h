@@ -248,6 +248,13 @@ int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, long long ro
  *   once to out_dtype (0 fp32, 1 bf16); N % 4 == 0, 16-byte aligned.  The split-K weight gradient's
  *   partial sum + cast (torch's part.sum(0).to(dtype) behind the blocks' Linear layers). */
 int pcops_sum_rows(const float *part, int S, long long N, void *out, int out_dtype, pcops_stream_t stream);
+/* pcops_wgrad_skinny: dw[co][ci] = sum_t g[t][co] * x[t][ci] for g (T, Co), x (T, Ci) bf16 row-major,
+ *   Ci == 6, Co % 8 == 0, Co <= 64 (EdgeConv's first 1x1 conv, models/model_utils.py:855-866: 2*3 edge
+ *   channels); fp32 accumulation in a fixed order, dw (Co, Ci) as fp32 (0) or bf16 (1).
+ *   workspace: pcops_wgrad_skinny_workspace_bytes(Co, Ci). */
+unsigned long long pcops_wgrad_skinny_workspace_bytes(int Co, int Ci);
+int pcops_wgrad_skinny(const void *g, const void *x, long long T, int Co, int Ci, void *dw, int dw_dtype,
+                       void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 unsigned long long pcops_colsum_workspace_bytes(long long rows, int C);
 int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype, void *workspace,
                  unsigned long long workspace_bytes, pcops_stream_t stream);

@@ -57,6 +57,16 @@ def _wgrad(g2, x2, wdt):
     weight dtype -- 2-4x faster at these shapes (tools/gemm_bench.py)."""
     T, Cout = g2.shape
     Cin = x2.shape[1]
+    if (Cin == 6 and Cout % 8 == 0 and Cout <= 64 and g2.is_cuda and g2.dtype == torch.bfloat16
+            and x2.dtype == torch.bfloat16 and wdt in _DT and g2.data_ptr() % 16 == 0):
+        # EdgeConv's 6 -> Cout conv: one streaming pass (as a split-K bmm it ran at 1.5 TFLOP/s)
+        out = torch.empty(Cout, Cin, dtype=wdt, device=g2.device)
+        wsb = lib().pcops_wgrad_skinny_workspace_bytes(Cout, Cin)
+        ws = _lib.Workspace.get(g2.device, wsb)
+        with torch.cuda.device(g2.device):
+            call("wgrad_skinny", lib().pcops_wgrad_skinny, ptr(g2), ptr(x2), T, Cout, Cin, ptr(out), _DT[wdt], ptr(ws),
+                 wsb, stream_of(g2))
+        return out
     if not _WGRAD_SPLITK:
         return (g2.t() @ x2).to(wdt)
     S = 16 if Cout * Cin <= (2 << 20) else 4
@@ -121,17 +131,26 @@ class _nullctx:
         return False
 
 
-def colsum(g):
-    """g.sum(0) of a (rows, C) CUDA tensor, same dtype: pcops_colsum (fp32 accumulation,
-    deterministic order) when C % 8 == 0, torch's reduction otherwise."""
+def colsum(g, out_dtype=None):
+    """g.sum(0) of a (rows, C) CUDA tensor (g's dtype unless out_dtype): pcops_colsum (fp32
+    accumulation, deterministic order) when C % 8 == 0 or a row fold makes it so, torch's
+    reduction otherwise."""
     rows, C = g.shape
+    if C % 8 and g.dtype in _DT and g.is_contiguous() and C < 64:
+        # narrow outputs (conv_out: C = 3): torch's reduction ran on 4 blocks (~100 us);
+        # fold k rows into one of k*C columns (k*C % 8 == 0), sum those in fp32, add the k groups
+        import math
+        k = 8 // math.gcd(C, 8)
+        if rows % k == 0 and rows >= k:
+            wide = colsum(g.view(rows // k, k * C), out_dtype=torch.float32)
+            return wide.view(k, C).sum(0).to(g.dtype)
     if C % 8 or g.dtype not in _DT or not g.is_contiguous():
         return g.sum(0)
-    out = torch.empty(C, dtype=g.dtype, device=g.device)
+    out = torch.empty(C, dtype=g.dtype if out_dtype is None else out_dtype, device=g.device)
     wsb = lib().pcops_colsum_workspace_bytes(rows, C)
     ws = _lib.Workspace.get(g.device, wsb)
     with torch.cuda.device(g.device):
-        call("colsum", lib().pcops_colsum, ptr(g), _dt(g), rows, C, ptr(out), _DT[g.dtype], ptr(ws), wsb,
+        call("colsum", lib().pcops_colsum, ptr(g), _dt(g), rows, C, ptr(out), _DT[out.dtype], ptr(ws), wsb,
              stream_of(g))
     return out
 

@@ -65,16 +65,29 @@ struct Stage {
   }
 };
 
+// XCD-aware tile order: block b runs on XCD b % 8 (round-robin dispatch), so tile
+// t = (b % 8) * per + b / 8 gives every XCD a contiguous run of tiles -- a tile and the
+// one below it (t + tiles-per-row) run back to back on one XCD and the shared halo
+// rows hit in that XCD's L2 instead of being fetched from HBM twice.
+__device__ __forceinline__ long long xcd_tile(long long b, long long tiles) {
+  const long long per = (tiles + 7) / 8;
+  return (b % 8) * per + b / 8;
+}
+
 // ---------------------------------------------------------------- forward / dgrad
 template <int CI, int CO, int TW>
 __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(const __bf16 *__restrict__ x,
                                                           const __bf16 *__restrict__ w, __bf16 *__restrict__ y,
-                                                          int H, int W) {
+                                                          int H, int W, int N) {
   constexpr int KC = (9 * CI + 31) / 32;  // K chunks of 32 over (tap, ci); the tail has zero weights
   constexpr int MT = CO / 16;
   constexpr int LW = TW + 2;
   __shared__ __attribute__((aligned(16))) __bf16 tile[(kTH + 2) * LW * CI];
-  const int n = blockIdx.z, h0 = blockIdx.y * kTH, w0 = blockIdx.x * TW;
+  const int tw = (W + TW - 1) / TW, th = (H + kTH - 1) / kTH;
+  const long long tiles = (long long)N * th * tw;
+  const long long t = xcd_tile(blockIdx.x, tiles);
+  if (t >= tiles) return;  // the grid is rounded up to a multiple of 8 blocks
+  const int n = (int)(t / ((long long)th * tw)), h0 = (int)((t / tw) % th) * kTH, w0 = (int)(t % tw) * TW;
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l >> 4, i16 = l & 15;
   // weight fragments and the input tile loads issued together (one memory latency)
   bf16x8 a[MT][KC];
@@ -156,13 +169,16 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(const __bf16 *__rest
     sx.load(x, n, by * kTH - 1, bx * kTW - 1, H, W);
     sg.load(dy, n, by * kTH, bx * kTW, H, W);
   };
-  if (blockIdx.x < tiles) fetch(blockIdx.x);
-  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+  // XCD x = blockIdx.x % 8 owns tiles [x*per, (x+1)*per), strided by its G/8 blocks
+  const long long per = (tiles + 7) / 8, lo = (blockIdx.x % 8) * per, hi = min(tiles, lo + per);
+  const long long t0 = lo + blockIdx.x / 8, ts = gridDim.x / 8;
+  if (t0 < hi) fetch(t0);
+  for (long long t = t0; t < hi; t += ts) {
     __syncthreads();  // the previous tile's LDS reads are done
     sx.store(xt);
     sg.store(gt);
     __syncthreads();
-    if (t + gridDim.x < tiles) fetch(t + gridDim.x);  // next tile's loads fly during this tile's MFMAs
+    if (t + ts < hi) fetch(t + ts);  // next tile's loads fly during this tile's MFMAs
 #pragma unroll
     for (int kc = 0; kc < kTW / 32; ++kc) {
       // pixels 32kc + 8g + (0..3 | 4..7) of row wv; lane 4q+p addresses row q, channels 4p..4p+3
@@ -341,8 +357,11 @@ __global__ __launch_bounds__(256) void conv3x3_c1_wgrad_kernel(const float *__re
       g1 = gp[1];
     }
   };
-  if (blockIdx.x < tiles) fetch(blockIdx.x);
-  for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+  // XCD x = blockIdx.x % 8 owns tiles [x*per, (x+1)*per), strided by its G/8 blocks
+  const long long per = (tiles + 7) / 8, lo = (blockIdx.x % 8) * per, hi = min(tiles, lo + per);
+  const long long t0 = lo + blockIdx.x / 8, ts = gridDim.x / 8;
+  if (t0 < hi) fetch(t0);
+  for (long long t = t0; t < hi; t += ts) {
     __syncthreads();  // the previous tile's LDS reads are done
 #pragma unroll
     for (int j = 0; j < XPER; ++j) {
@@ -351,7 +370,7 @@ __global__ __launch_bounds__(256) void conv3x3_c1_wgrad_kernel(const float *__re
     }
     const bf16x8 c0 = g0, c1 = g1;
     __syncthreads();
-    if (t + gridDim.x < tiles) fetch(t + gridDim.x);
+    if (t + ts < hi) fetch(t + ts);
     float v[9];
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) v[tp] = tile[(r + tp / 3) * (kTW + 2) + c + tp % 3];
@@ -388,15 +407,16 @@ extern "C" int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int
   // 112-column tiles where they divide W exactly (the 224 / 112 images): no masked N-tiles
   const bool wide = W % 112 == 0;
   const int TW = wide ? 112 : 64;
-  const dim3 grid((W + TW - 1) / TW, (H + kTH - 1) / kTH, N);
+  const long long tiles = (long long)((W + TW - 1) / TW) * ((H + kTH - 1) / kTH) * N;
+  const dim3 grid((unsigned)(((tiles + 7) / 8) * 8));  // 1-D tile space, rounded up to 8 (XCD order)
   const __bf16 *xp = (const __bf16 *)x, *wp = (const __bf16 *)w;
   __bf16 *yp = (__bf16 *)y;
   if (C == 16) {
-    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
-    else hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
+    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
   } else {
-    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
-    else hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W);
+    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
   }
   PC_CHECK_LAUNCH();
   return PCOPS_OK;

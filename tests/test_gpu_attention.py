@@ -315,7 +315,8 @@ def test_linear_splitk_wgrad(dev, amp, cin, cout, T):
 
 @pytest.mark.parametrize("rows,C,dtype", [
     (65536, 512, torch.bfloat16), (8192, 1024, torch.bfloat16), (1000, 8, torch.bfloat16),
-    (4099, 24, torch.float32), (3, 1032, torch.float32), (70000, 64, torch.float32), (0, 64, torch.bfloat16)])
+    (4099, 24, torch.float32), (3, 1032, torch.float32), (70000, 64, torch.float32), (0, 64, torch.bfloat16),
+    (524288, 3, torch.bfloat16), (65536, 3, torch.float32), (1001, 3, torch.bfloat16), (4096, 6, torch.bfloat16)])
 def test_colsum_matches_float64(dev, rows, C, dtype):
     """pcops_colsum (the blocks' bias gradient) vs a float64 column sum; fp32
     accumulation in a fixed order, so two calls agree bitwise."""
@@ -334,10 +335,12 @@ def test_colsum_matches_float64(dev, rows, C, dtype):
 
 
 @pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("T,Cout,Cin", [(65536, 512, 512), (16384, 768, 256), (8192, 1024, 512)])
+@pytest.mark.parametrize("T,Cout,Cin", [(65536, 512, 512), (16384, 768, 256), (8192, 1024, 512),
+                                        (32 * 2048 * 16, 32, 6), (1000, 64, 6)])
 def test_split_k_wgrad_matches_float64(dev, wdt, T, Cout, Cin):
     """The blocks' split-K weight gradient (bmm partials + pcops_sum_rows: fixed-order sum,
-    one rounding) vs float64 g^T x: within fp32 accumulation error (+ one bf16 rounding)."""
+    one rounding) -- and EdgeConv's 6-channel one (pcops_wgrad_skinny) -- vs float64 g^T x:
+    within fp32 accumulation error (+ one bf16 rounding)."""
     from svdformer_pointsea_amd import attention
 
     g = torch.Generator(device=dev).manual_seed(T + Cout)

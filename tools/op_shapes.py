@@ -44,6 +44,31 @@ torch.cuda.synchronize()
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
     step()
     torch.cuda.synchronize()
+if os.environ.get("GEMM_TABLE"):
+    # device time per (GEMM op, input shapes) with the achieved TFLOP/s
+    import math
+    rowsk = []
+    for k in prof.key_averages(group_by_input_shape=True):
+        if not re.match(r"^aten::(mm|addmm|bmm|linear|matmul|_addmm_activation|baddbmm)$", k.key):
+            continue
+        t = k.device_time_total / 1e3  # ms
+        shp = k.input_shapes
+        try:
+            if k.key in ("aten::mm", "aten::addmm"):
+                a, b = (shp[0], shp[1]) if k.key == "aten::mm" else (shp[1], shp[2])
+                fl = 2.0 * a[0] * a[1] * b[1]
+            elif k.key in ("aten::bmm", "aten::baddbmm"):
+                a, b = (shp[0], shp[1]) if k.key == "aten::bmm" else (shp[1], shp[2])
+                fl = 2.0 * a[0] * a[1] * a[2] * b[2]
+            else:
+                fl = float("nan")
+        except Exception:
+            fl = float("nan")
+        rowsk.append((t, k.key, str(shp)[:70], k.count, fl))
+    for t, key, shp, n, fl in sorted(rowsk, reverse=True)[:rows]:
+        tf = fl * n / (t * 1e-3) / 1e12 if t > 0 and not math.isnan(fl) else float("nan")
+        print(f"{t:8.3f} ms {n:4d}x {key:14s} {shp:70s} {tf:7.1f} TFLOP/s")
+    sys.exit(0)
 # parent of each matching op: the enclosing op / autograd node on the CPU timeline
 evs = [e for e in prof.events() if e.device_type.name == "CPU"]
 counts = {}
