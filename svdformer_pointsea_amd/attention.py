@@ -582,7 +582,7 @@ _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnost
 # runs with it on ended with a non-finite loss in the timed steps, cause not
 # found (identical-input gradients match the separate colsum to bf16 noise,
 # and 50 graph replays without the optimizer stayed finite)
-_GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "0") == "1"
+_GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
 
 
 def _pos_tokens(pos):
