@@ -224,6 +224,12 @@ def kernel_work(name, a):
         return float(a[2] * a[4] * ((a[3] + 1) * es(a[1]) + 1)), "GB/s", HBM_PEAK, "hbm"
     if name == "max_k_grad":     # g, dt, arg, rows, K, C, gx: read g + argmax, write the K rows
         return float(a[3] * a[5] * ((a[4] + 1) * es(a[1]) + 1)), "GB/s", HBM_PEAK, "hbm"
+    if name == "sum_rows":       # part, S, N, out, odt: read S fp32 rows, write one
+        return float(a[1] * a[2] * 4 + a[2] * es(a[4])), "GB/s", HBM_PEAK, "hbm"
+    if name == "wgrad_skinny":   # g, x, T, Co, Ci: read both operands once
+        return float(a[2] * (a[3] + a[4]) * 2), "GB/s", HBM_PEAK, "hbm"
+    if name in ("conv3x3_c1_fwd", "conv3x3_c1_wgrad"):  # x, w|dy, N, H, W: fp32 image + 16-ch bf16 map
+        return float(a[2] * a[3] * a[4] * (4 + 32)), "GB/s", HBM_PEAK, "hbm"
     if name == "gelu_bwd":       # dy, u, dt, rows, C, du: read dy and u, write du
         return float(3 * a[3] * a[4] * es(a[2])), "GB/s", HBM_PEAK, "hbm"
     if name == "points2depth":   # points, rot, trans, B, N, V, H, W: read the cloud, accumulate 8 B / pixel
@@ -242,13 +248,23 @@ def kernel_work(name, a):
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
             "attention bwd dkv": "attn_dkv2_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
             "chamfer_3D.forward": "chamfer_(nn|screen)_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
-            "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel", "colsum": "colsum",
+            "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",
+            "colsum": ("colsum", "colsum_partial"),
             "transpose_add": "transpose_add", "pcsa_forward": "pcsa_fwd", "pcsa_backward": "pcsa_bwd",
             "gather_points": "gather_kernel", "gather_points_grad": "gather_grad_kernel",
             "group_points": "group_kernel", "group_points_grad": "group_grad_kernel",
             "chamfer_3D.backward": "chamfer_grad", "points2depth": "depth_", "points2grid": "points2grid",
             "grid2image": "grid2image|image_normalize", "sa_group": "sa_group_kernel",
-            "sa_group_grad": "sa_group_grad_kernel"}
+            "sa_group_grad": "sa_group_grad_kernel",
+            # calls that launch several kernels: (every kernel of the call, the one launched once per call)
+            "batchnorm_fwd": (r"bn_partial_kernel<\d, 0>|bn_final_kernel<0|bn_apply_kernel|bn_eval_coef",
+                              r"bn_apply_kernel"),
+            "batchnorm_bwd": (r"bn_partial_kernel<\d, [123]>|bn_final_kernel<1|bn_bwd_apply_kernel",
+                              r"bn_bwd_apply_kernel"),
+            "conv3x3_fwd": r"conv3x3_fwd_kernel", "conv3x3_dgrad": r"conv3x3_fwd_kernel",
+            "conv3x3_wgrad": (r"conv3x3_wgrad_kernel|conv3x3_wgrad_reduce", r"conv3x3_wgrad_kernel"),
+            "add": r"add_kernel", "max_k": r"max_k_kernel", "max_k_grad": r"max_k_grad_kernel",
+            "gelu_bwd": (r"gelu_bwd_partial_kernel|colsum_final", r"gelu_bwd_partial_kernel")}
 
 
 def pmc_traffic(path, key, name):
@@ -258,11 +274,16 @@ def pmc_traffic(path, key, name):
     if not path or not os.path.exists(path) or name not in _SYMBOLS:
         return None
     pat = _SYMBOLS[name]
+    prim = None
+    if isinstance(pat, tuple):   # several kernels per call: their bytes summed per launch of `prim`
+        pat, prim = pat
     m = re.search(r"D=(\d+)", key)
     if m:  # attention kernels are instantiated per head dim: <D, ...> / ILiDE
         pat += r"(<|ILi)%s(,|E)" % m.group(1)
-    rows = [v for k, v in json.load(open(path)).items() if re.search(pat, k)]
-    n = sum(r["launches"] for r in rows)
+    table = json.load(open(path))
+    rows = [v for k, v in table.items() if re.search(pat, k)]
+    n = sum(r["launches"] for r in rows) if prim is None else \
+        sum(v["launches"] for k, v in table.items() if re.search(prim, k))
     return sum(r["hbm_bytes_per_launch"] * r["launches"] for r in rows) / n if n else None
 
 

@@ -22,7 +22,7 @@ set -o pipefail
 OUT=${1:?out dir}; shift
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-PMC_RE='attn_|ln_|fps_|chamfer_|knn|colsum|pcsa|gather|group|depth|points2|grid2|transpose_add'
+PMC_RE='attn_|ln_|fps_|chamfer_|knn|colsum|pcsa|gather|group|depth|points2|grid2|transpose_add|bn_|conv3x3|sum_rows|wgrad_skinny|max_k|add_kernel|gelu_bwd'
 run_stage() {
   case "$1" in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
