@@ -536,11 +536,26 @@ __global__ __launch_bounds__(256) void sum_rows_kernel(const float *__restrict__
                                                        long long N, void *__restrict__ out, int odt) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n4) return;
-  float4 acc = *reinterpret_cast<const float4 *>(part + 4 * i);
-  for (int r = 1; r < S; ++r) {
+  // four rows' loads in flight; rows summed in a fixed order (r, r+1, r+2, r+3 into four partials)
+  float4 a[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int r = 0;
+  for (; r + 3 < S; r += 4)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 v = *reinterpret_cast<const float4 *>(part + (long long)(r + j) * N + 4 * i);
+      a[j].x += v.x, a[j].y += v.y, a[j].z += v.z, a[j].w += v.w;
+    }
+  for (; r < S; ++r) {
     const float4 v = *reinterpret_cast<const float4 *>(part + (long long)r * N + 4 * i);
-    acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+    a[0].x += v.x, a[0].y += v.y, a[0].z += v.z, a[0].w += v.w;
   }
+  float4 acc;
+  acc.x = (a[0].x + a[1].x) + (a[2].x + a[3].x);
+  acc.y = (a[0].y + a[1].y) + (a[2].y + a[3].y);
+  acc.z = (a[0].z + a[1].z) + (a[2].z + a[3].z);
+  acc.w = (a[0].w + a[1].w) + (a[2].w + a[3].w);
   if (odt == 0) {
     *reinterpret_cast<float4 *>(reinterpret_cast<float *>(out) + 4 * i) = acc;
   } else {
@@ -549,6 +564,32 @@ __global__ __launch_bounds__(256) void sum_rows_kernel(const float *__restrict__
     o[0] = (__bf16)acc.x, o[1] = (__bf16)acc.y, o[2] = (__bf16)acc.z, o[3] = (__bf16)acc.w;
     *reinterpret_cast<bf16x4_t *>(reinterpret_cast<__bf16 *>(out) + 4 * i) = o;
   }
+}
+
+// stage 1 of a long row sum: part2[y][i] = sum_{s = y, y + P, ...} part[s][i] (grid.y = P slices),
+// eight independent loads in flight per thread (a single pass over 512 rows was latency-bound)
+__global__ __launch_bounds__(256) void sum_rows_split_kernel(const float *__restrict__ part, int S, long long n4,
+                                                             long long N, float *__restrict__ part2) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int P = gridDim.y;
+  float4 a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int r = blockIdx.y;
+  for (; r + 7 * P < S; r += 8 * P)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 v = *reinterpret_cast<const float4 *>(part + (long long)(r + j * P) * N + 4 * i);
+      a[j].x += v.x, a[j].y += v.y, a[j].z += v.z, a[j].w += v.w;
+    }
+  for (; r < S; r += P) {
+    const float4 v = *reinterpret_cast<const float4 *>(part + (long long)r * N + 4 * i);
+    a[0].x += v.x, a[0].y += v.y, a[0].z += v.z, a[0].w += v.w;
+  }
+#pragma unroll
+  for (int j = 1; j < 8; ++j) a[0].x += a[j].x, a[0].y += a[j].y, a[0].z += a[j].z, a[0].w += a[j].w;
+  *reinterpret_cast<float4 *>(part2 + (long long)blockIdx.y * N + 4 * i) = a[0];
 }
 
 // Weight gradient of a skinny 1x1 conv / Linear (EdgeConv's first conv: 6 -> 32 channels
@@ -854,8 +895,10 @@ extern "C" int pcops_sum_rows(const float *part, int S, long long N, void *out, 
 
 constexpr int kSkinnyBlocks = 512;
 
+constexpr int kSkinnySplit = 32;
+
 extern "C" unsigned long long pcops_wgrad_skinny_workspace_bytes(int Co, int Ci) {
-  return (unsigned long long)kSkinnyBlocks * Co * Ci * sizeof(float);
+  return (unsigned long long)(kSkinnyBlocks + kSkinnySplit) * Co * Ci * sizeof(float);
 }
 
 extern "C" int pcops_wgrad_skinny(const void *g, const void *x, long long T, int Co, int Ci, void *dw, int dw_dtype,
@@ -874,9 +917,12 @@ extern "C" int pcops_wgrad_skinny(const void *g, const void *x, long long T, int
   float *part = (float *)workspace;
   hipLaunchKernelGGL(wgrad_skinny_kernel<6>, dim3(blocks), dim3(256), 0, s, (const __bf16 *)g, (const __bf16 *)x, T, Co,
                      rpb, part);
-  const long long n4 = (long long)Co * Ci / 4;
-  hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, part, blocks, n4,
-                     (long long)Co * Ci, dw, dw_dtype);
+  const long long N = (long long)Co * Ci, n4 = N / 4;
+  float *part2 = part + (long long)kSkinnyBlocks * N;
+  hipLaunchKernelGGL(sum_rows_split_kernel, dim3((unsigned)((n4 + 255) / 256), kSkinnySplit), dim3(256), 0, s, part,
+                     blocks, n4, N, part2);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, part2, kSkinnySplit, n4, N,
+                     dw, dw_dtype);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

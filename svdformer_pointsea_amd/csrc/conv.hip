@@ -41,14 +41,14 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8 &a, const bf16x8 &b, const 
 // tile instead of one per 16-B vector) and can prefetch the next tile while it
 // computes.  A rectangle of R rows x L columns x C channels starting at (hb, wb)
 // of image n is held as [row][col][C] bf16; outside the image reads as zero.
-template <int C, int R, int L>
+template <int C, int R, int L, int NTH = 256>
 struct Stage {
-  static constexpr int VPP = C / 8, TOT = R * L * VPP, PER = (TOT + 255) / 256;
+  static constexpr int VPP = C / 8, TOT = R * L * VPP, PER = (TOT + NTH - 1) / NTH;
   bf16x8 v[PER];
   __device__ __forceinline__ void load(const __bf16 *__restrict__ x, int n, int hb, int wb, int H, int W) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int i = threadIdx.x + 256 * j;
+      const int i = threadIdx.x + NTH * j;
       const int vv = i % VPP, pc = i / VPP, c = pc % L, r = pc / L;
       const int hh = hb + r, ww = wb + c;
       v[j] = bf16x8{};
@@ -59,7 +59,7 @@ struct Stage {
   __device__ __forceinline__ void store(__bf16 *tile) const {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int i = threadIdx.x + 256 * j;
+      const int i = threadIdx.x + NTH * j;
       if (i < TOT) *reinterpret_cast<bf16x8 *>(tile + 8 * i) = v[j];
     }
   }
@@ -236,6 +236,96 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(const __bf16 *__rest
 #endif
 }
 
+// Weight gradient for C = 32 in 3-wave blocks, wave w = kernel row dh: its 3 taps for
+// all 4 tile rows (12 accumulator tiles instead of 36 per wave, so three blocks share a CU
+// where the one-row-per-wave form held one 4-wave block at 312 VGPRs).
+template <int CI, int CO>
+__global__ __launch_bounds__(192) void conv3x3_wgrad3_kernel(const __bf16 *__restrict__ x,
+                                                             const __bf16 *__restrict__ dy, int N, int H, int W,
+                                                             float *__restrict__ part) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int MT = CO / 16, NT = CI / 16;
+  constexpr int kXT = (kTH + 2) * kLW * CI, kGT = kTH * kTW * CO, kE = 9 * CO * CI;
+  constexpr int kBytes = (2 * (kXT + kGT) > 4 * kE ? 2 * (kXT + kGT) : 4 * kE);
+  __shared__ float4 arena[(kBytes + 15) / 16];
+  __bf16 *xt = reinterpret_cast<__bf16 *>(arena);
+  __bf16 *gt = xt + kXT;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  const int l = threadIdx.x & 63, dh = threadIdx.x >> 6, g = l >> 4, i16 = l & 15, q = i16 >> 2, p = i16 & 3;
+  const int tw = (W + kTW - 1) / kTW, th = (H + kTH - 1) / kTH;
+  const long long tiles = (long long)N * th * tw;
+  f32x4 acc[3][MT][NT];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[t][mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Stage<CI, kTH + 2, kLW, 192> sx;
+  Stage<CO, kTH, kTW, 192> sg;
+  auto fetch = [&](long long t) {
+    const int bx = (int)(t % tw);
+    const long long r = t / tw;
+    const int by = (int)(r % th), n = (int)(r / th);
+    sx.load(x, n, by * kTH - 1, bx * kTW - 1, H, W);
+    sg.load(dy, n, by * kTH, bx * kTW, H, W);
+  };
+  const long long per = (tiles + 7) / 8, lo = (blockIdx.x % 8) * per, hi = min(tiles, lo + per);
+  const long long t0 = lo + blockIdx.x / 8, ts = gridDim.x / 8;
+  if (t0 < hi) fetch(t0);
+  for (long long t = t0; t < hi; t += ts) {
+    __syncthreads();
+    sx.store(xt);
+    sg.store(gt);
+    __syncthreads();
+    if (t + ts < hi) fetch(t + ts);
+#pragma unroll
+    for (int row = 0; row < kTH; ++row)
+#pragma unroll
+      for (int kc = 0; kc < kTW / 32; ++kc) {
+        const int px0 = 32 * kc + 8 * g + q;
+        bf16x8 a[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const __bf16 *base = gt + (row * kTW + px0) * CO + 16 * mt + 4 * p;
+          const short4v lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)base);
+          const short4v hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(base + 4 * CO));
+          a[mt] = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo4), __builtin_bit_cast(bf16x4, hi4), 0, 1, 2,
+                                          3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            const __bf16 *base = xt + ((row + dh) * kLW + px0 + dw) * CI + 16 * nt + 4 * p;
+            const short4v lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)base);
+            const short4v hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(base + 4 * CI));
+            const bf16x8 b = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo4), __builtin_bit_cast(bf16x4, hi4),
+                                                     0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[dw][mt][nt] = mfma16(a[mt], b, acc[dw][mt][nt]);
+          }
+      }
+  }
+  // each wave owns taps 3*dh .. 3*dh+2: disjoint slots, one write each
+  __syncthreads();
+  float *red = reinterpret_cast<float *>(arena);
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = 16 * mt + 4 * g + r, ci = 16 * nt + i16;
+          red[(co * 9 + 3 * dh + dw) * CI + ci] = acc[dw][mt][nt][r];
+        }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kE; i += 192) part[(long long)blockIdx.x * kE + i] = red[i];
+#endif
+}
+
 // dw = sum over blocks of part[b][co][tap][ci] in two fixed-order stages (a
 // single pass had each thread walk all block rows: ~1 us of latency per 8 rows):
 //   reduce1: part2[s][e] = sum_{b = s, s + kSplit, ...} part[b][e]       grid (E/256, kSplit)
@@ -272,7 +362,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_reduce2_kernel(const float 
     reinterpret_cast<__bf16 *>(out)[o] = (__bf16)v;
 }
 
-int wgrad_blocks(int C) { return C <= 16 ? 1024 : 512; }
+int wgrad_blocks(int C) { return C <= 16 ? 1024 : 768; }
 
 bool conv_ok(int N, int H, int W, int C) { return N > 0 && H > 0 && W > 0 && (C == 16 || C == 32); }
 
@@ -445,7 +535,7 @@ extern "C" int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, 
     hipLaunchKernelGGL((conv3x3_wgrad_kernel<16, 16>), dim3(G), dim3(256), 0, s, (const __bf16 *)x,
                        (const __bf16 *)dy, N, H, W, part);
   else
-    hipLaunchKernelGGL((conv3x3_wgrad_kernel<32, 32>), dim3(G), dim3(256), 0, s, (const __bf16 *)x,
+    hipLaunchKernelGGL((conv3x3_wgrad3_kernel<32, 32>), dim3(G), dim3(192), 0, s, (const __bf16 *)x,
                        (const __bf16 *)dy, N, H, W, part);
   float *part2 = part + (long long)G * 9 * C * C;
   const int E = 9 * C * C;
