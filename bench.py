@@ -516,7 +516,11 @@ def heartbeat(every=30.0):
     threading.Thread(target=beat, daemon=True).start()
 
 
+_RESULT_FD = None   # the original stdout when library banners are diverted (distributed runs)
+
+
 def main():
+    global _RESULT_FD
     args = parse()
     heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -524,6 +528,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_dist = world > 1 or args.dist_selftest
     if use_dist:
+        # RCCL prints its version banner on stdout at communicator set-up; stdout must carry
+        # exactly one JSON line, so fd 1 points at stderr from here and the line goes to the
+        # saved original
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
         torch.cuda.set_device(local)
         if args.dist_selftest and "MASTER_ADDR" not in os.environ:
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
@@ -792,7 +802,12 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             progress(f"timed {out['ms_per_step']:.2f} ms/step; CPU baseline")
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_steps)
-        print(json.dumps(out), flush=True)
+        line = json.dumps(out) + "\n"
+        if _RESULT_FD is not None:
+            sys.stdout.flush()
+            os.write(_RESULT_FD, line.encode())
+        else:
+            print(line, end="", flush=True)
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
