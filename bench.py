@@ -75,6 +75,11 @@ def parse():
     ap.add_argument("--dist-selftest", action="store_true",
                     help="initialise an RCCL process group even at N=1 (exercises the collective path "
                          "and its graph capture on a one-GPU box)")
+    ap.add_argument("--no-extra-legs", action="store_true",
+                    help="skip the fp32 PCN train step and the PointSea ShapeNet-55 train step reported beside "
+                         "the headline (N = 1 only)")
+    ap.add_argument("--dry-run-launch", action="store_true",
+                    help="with --gpus N > 1 outside torch.distributed.run: print the rank launcher's argv and exit")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r2_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
@@ -519,63 +524,72 @@ def heartbeat(every=30.0):
 _RESULT_FD = None   # the original stdout when library banners are diverted (distributed runs)
 
 
-def main():
-    global _RESULT_FD
-    args = parse()
-    heartbeat()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_dist = world > 1 or args.dist_selftest
-    if use_dist:
-        # RCCL prints its version banner on stdout at communicator set-up; stdout must carry
-        # exactly one JSON line, so fd 1 points at stderr from here and the line goes to the
-        # saved original
-        sys.stdout.flush()
-        _RESULT_FD = os.dup(1)
-        os.dup2(2, 1)
-        torch.cuda.set_device(local)
-        if args.dist_selftest and "MASTER_ADDR" not in os.environ:
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-    # MIOpen picks the fastest conv algorithm per shape during the warm-up
-    # steps (the image branch's NHWC convs: 14 -> 11 ms fwd+bwd)
-    torch.backends.cudnn.benchmark = True
+def _free_port():
+    import socket
 
-    import svdformer_pointsea_amd as pkg
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_argv(argv, n, port):
+    """The command `python bench.py --gpus N ...` (no WORLD_SIZE in the environment)
+    runs as: one rank per GPU under torch.distributed.run on this node, the same
+    arguments, rendezvous on 127.0.0.1 (the reference's counterpart is
+    DataParallel over the node's GPUs, core/train_pcn.py:53-54)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def self_launch(args):
+    """Start the N ranks as a child process (this process has not touched the GPU)
+    and return its exit code; rank 0's JSON line reaches this stdout directly."""
+    import subprocess
+
+    cmd = launch_argv(sys.argv[1:], args.gpus, _free_port())
+    if args.dry_run_launch:
+        print(json.dumps({"launch": cmd}))
+        return 0
+    progress(f"launching {args.gpus} ranks: {' '.join(cmd)}")
+    sys.stdout.flush()
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+class Leg:
+    """One timed train-step measurement (model, flat parameters, optimizer,
+    captured graphs, timings)."""
+
+
+def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist, kernel_timing, tag):
+    """Build wl's model, warm up, capture the step into HIP graphs (unless
+    --no-graph) and time `steps` steps between barrier + synchronize pairs.
+    Kernel timing (HIP events per libpcops launch) runs as eager steps after
+    the timed replays; a non-finite loss anywhere -- warm-up, timed replays or
+    the eager timing steps -- fails the run."""
     from svdformer_pointsea_amd import _lib
-    from svdformer_pointsea_amd.train import FlatParams
+    from svdformer_pointsea_amd.train import BucketedAllReduce, FlatParams, TrainSchedule
 
-    pkg.lib()  # fail loudly if libpcops.so is missing
-    tuned = setup_tunableop(args.tunableop, args.model, rank)
-    wl = Workload(args.model)
-    if args.batch is None:
-        args.batch = wl.batch
+    L = Leg()
     torch.manual_seed(0)  # identical init on every rank
     model = wl.Model(wl.cfg).to(device)
-    nparams = sum(p.numel() for p in model.parameters())
-    amp = not args.fp32
+    L.model, L.nparams = model, sum(p.numel() for p in model.parameters())
     # flat fp32 master weights + gradient bucket, bf16 shadows of the GEMM/conv
     # weights refreshed by one cast per step (svdformer_pointsea_amd/train.py)
-    fp = FlatParams(model, device, bf16=amp)
-    use_graph = not args.no_graph
-    # one parameter group, elementwise update: Adam over the flat master buffer
+    fp = L.fp = FlatParams(model, device, bf16=amp)
+    use_graph = L.use_graph = not args.no_graph
+    # one parameter group, elementwise update: Adam over the flat master buffer;
     # the LR is a device tensor so the captured optimizer graph reads the value
     # the schedule writes each step (warm-up per batch, train_pcn.py:132-134)
     opt = wl.optimizer([fp.master()], lr=torch.tensor(1e-4, device=device) if use_graph else 1e-4, fused=True,
                        capturable=use_graph)
-    from svdformer_pointsea_amd.train import TrainSchedule
-    schedule = TrainSchedule(opt, args.model)
-    partial, gt = wl.synth(args.batch, 1000 + rank, device)
+    schedule = TrainSchedule(opt, wl.name)
+    partial, gt = wl.synth(batch, 1000 + rank, device)
+    L.partial, L.gt = partial, gt
     # ShapeNet-55 re-crops its partial input from gt inside the step; the crop
     # draws come from the device's default generator (graph-capturable)
-    crop_rng = torch.cuda.default_generators[device.index] if args.model == "pointsea" else None
+    crop_rng = torch.cuda.default_generators[device.index] if wl.name == "pointsea" else None
     loss_acc = torch.zeros((), device=device)
-    progress(f"{args.model}: {nparams} parameters; eager warm-up (MIOpen algorithm search)")
-
-    from svdformer_pointsea_amd.train import BucketedAllReduce
+    progress(f"[{tag}] {wl.name} B={batch} {'bf16' if amp else 'fp32'}: {L.nparams} parameters; eager warm-up")
     sync = [BucketedAllReduce(fp, world, bucket_mb=args.bucket_mb) if use_dist and args.overlap == "auto" else None]
 
     def fwd_bwd():
@@ -583,7 +597,7 @@ def main():
         fp.refresh()
         # the loss's gt FPS chain depends on gt only: it runs on a second
         # stream beside the whole forward pass (FPS occupies B CUs)
-        with _lib.fork(device, lane=1) as br:
+        with _lib.fork(device, lane=1, inputs=(gt,)) as br:
             gts = wl.gt_pyramid(gt)
         inp = wl.inputs(partial, gt, crop_rng)
         depth = wl.images(inp)
@@ -607,20 +621,29 @@ def main():
         opt.step()
         schedule.batch_end()
 
+    def check_finite(what):
+        v = loss_acc.item()
+        if not math.isfinite(v):
+            names = [n for n, q in model.named_parameters() if not torch.isfinite(q.detach()).all()]
+            progress(f"[{tag}] non-finite running loss after {what}; master finite "
+                     f"{bool(torch.isfinite(fp.flat).all())}, grad finite {bool(torch.isfinite(fp.grad).all())}; "
+                     f"{len(names)} parameters non-finite, first: {names[:6]}")
+            raise RuntimeError(f"non-finite loss ({tag}, {what})")
+
     if use_graph:
         # The host cannot issue the ~3k launches of a step faster than the GPU
         # runs them (host_issue_ms_per_step), so the step is captured once
-        # into two HIP graphs (forward+backward, Adam) after eager warm-up on
-        # a side stream (MIOpen algorithm search, lazy state); the gradient
-        # all-reduce stays an eager RCCL call between the two replays.
+        # into two HIP graphs (forward+backward, optimizer) after eager
+        # warm-up on a side stream (MIOpen algorithm search, lazy state)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for _ in range(max(args.warmup, 2)):
+            for _ in range(max(warmup, 2)):
                 eager_step()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        progress("eager warm-up done; capturing the step")
+        check_finite("the eager warm-up")
+        progress(f"[{tag}] eager warm-up done; capturing the step")
         g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         # RCCL's watchdog thread polls the warm-up collectives' events; under
         # "global" capture such a call from another thread invalidates the
@@ -632,21 +655,30 @@ def main():
             torch.cuda.synchronize()
             time.sleep(1.0)
             cap_mode = "thread_local"
+        captured, err = True, None
         try:
             with torch.cuda.graph(g_fb, capture_error_mode=cap_mode):
                 fwd_bwd()
         except RuntimeError as exc:
             if sync[0] is None:
                 raise
-            # the collectives could not be captured: one all-reduce between replays
-            progress(f"capture with in-graph all-reduce failed ({exc}); single all-reduce after the replay")
-            for h in sync[0]._hooks:
-                h.remove()
-            sync[0] = None
-            torch.cuda.synchronize()
-            g_fb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_fb):
-                fwd_bwd()
+            captured, err = False, exc
+        if sync[0] is not None:
+            # every rank must run the same collective schedule: the in-graph bucketed
+            # all-reduces only if EVERY rank captured them (agreed over a host group,
+            # outside any capture); otherwise every rank drops them together
+            flag = torch.tensor([1 if captured else 0], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=host_group())
+            if int(flag.item()) == 0:
+                progress(f"[{tag}] in-graph all-reduce not captured on every rank "
+                         f"(this rank: {err or 'ok'}); one all-reduce after each replay on all ranks")
+                for h in sync[0]._hooks:
+                    h.remove()
+                sync[0] = None
+                torch.cuda.synchronize()
+                g_fb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_fb):
+                    fwd_bwd()
         with torch.cuda.graph(g_opt):
             opt.step()
 
@@ -658,77 +690,136 @@ def main():
         span_steps = args.timing_steps
     else:
         step = eager_step
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             step()
-        if not args.no_kernel_timing:
+        check_finite("the eager warm-up")
+        if kernel_timing:
             _lib.KernelTimer.enable()
-        span_steps = args.steps
+        span_steps = steps
 
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
-    progress(f"timing {args.steps} steps")
-    loss_hist = [loss_acc.clone()]   # running loss after the warm-up and after each timed step (no host sync)
+    progress(f"[{tag}] timing {steps} steps")
     t0 = time.perf_counter()
     host = 0.0  # time the host spends issuing a step (launches are asynchronous)
-    for _ in range(args.steps):
+    for _ in range(steps):
         h0 = time.perf_counter()
         step()
-        loss_hist.append(loss_acc.clone())
         host += time.perf_counter() - h0
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    timed_loss = loss_hist[-1].item()   # running loss through the last timed step
-    timing_nonfinite = False
-    if use_graph and not args.no_kernel_timing:
+    check_finite("the timed steps")
+    if use_graph and kernel_timing:
         # ROCm torch refuses timing events inside a captured graph ("External
         # events are disallowed in rocm"), so the per-launch HIP events come
         # from eager steps of the same work right after the timed replays --
-        # on a side stream, like the warm-up
+        # on a side stream, like the warm-up.  They are real train steps: a
+        # non-finite loss there fails the run like one in the replays.
         _lib.KernelTimer.enable()
         tstream = torch.cuda.Stream()
         tstream.wait_stream(torch.cuda.current_stream())
-        before = loss_acc.clone()
-        master_before = fp.flat.clone()
         with torch.cuda.stream(tstream):
             for _ in range(args.timing_steps):
                 eager_step()
         torch.cuda.current_stream().wait_stream(tstream)
         torch.cuda.synchronize()
-        # the timing steps only supply kernel durations: a non-finite loss there is reported,
-        # not fatal (the timed replays above are what `value` measures)
-        timing_nonfinite = math.isfinite(before.item()) and not math.isfinite(loss_acc.item())
-        if timing_nonfinite:
-            progress("WARNING: non-finite loss in the eager kernel-timing steps after the timed replays; "
-                     "master weights restored for the configs[1] leg")
-            fp.flat.copy_(master_before)
-        del master_before
-    spans = _lib.KernelTimer.spans or {}
+        check_finite("the eager kernel-timing steps")
+    L.spans = _lib.KernelTimer.spans or {}
     _lib.KernelTimer.disable()
     if use_dist:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    if not math.isfinite(timed_loss):
-        # where it started: the first non-finite running loss (0 = warm-up), and which
-        # flat buffers / parameters carry non-finite values now
-        hist = torch.stack(loss_hist).cpu()
-        bad = [i for i, v in enumerate(hist.tolist()) if not math.isfinite(v)] or [len(hist)]
-        names = [n for n, q in model.named_parameters()
-                 if not torch.isfinite(q.detach()).all() or (q.grad is not None and not torch.isfinite(q.grad).all())]
-        progress(f"non-finite running loss from snapshot {bad[0]} of {len(hist)} (0 = after warm-up); "
-                 f"master finite {bool(torch.isfinite(fp.flat).all())}, grad finite {bool(torch.isfinite(fp.grad).all())}; "
-                 f"{len(names)} parameters non-finite, first: {names[:6]}")
-        raise RuntimeError("non-finite loss in the timed steps")
+    L.elapsed, L.host, L.span_steps, L.sync = elapsed, host, span_steps, sync[0]
+    L.ms_per_step = elapsed * 1e3 / steps
+    return L
+
+
+_HOST_GROUP = [None]
+
+
+def host_group():
+    """A gloo group over the same ranks for host-side agreement (created collectively at start-up)."""
+    return _HOST_GROUP[0]
+
+
+def extra_leg(args, name, batch, amp, device, steps):
+    """A second train-step figure beside the headline (rank 0, N = 1)."""
+    wl = Workload(name)
+    setup_tunableop(args.tunableop, name, 0)
+    leg = train_leg(args, wl, batch, amp, steps, 2, device, 1, 0, False, False, name + ("" if amp else "-fp32"))
+    out = {"workload": wl.desc, "batch": batch, "dtype": "bf16" if amp else "f32", "steps": steps,
+           "ms_per_step": round(leg.ms_per_step, 3), "samples_per_s": round(batch * 1e3 / leg.ms_per_step, 2),
+           "execution": "hip_graph" if leg.use_graph else "eager"}
+    del leg
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    global _RESULT_FD
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: one rank per GPU, started before anything touches the GPU
+        sys.exit(self_launch(args))
+    heartbeat()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; the line would misreport n_gpus")
+    use_dist = world > 1 or args.dist_selftest
+    if use_dist:
+        # RCCL prints its version banner on stdout at communicator set-up; stdout must carry
+        # exactly one JSON line, so fd 1 points at stderr from here and the line goes to the
+        # saved original
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
+        torch.cuda.set_device(local)
+        if args.dist_selftest and "MASTER_ADDR" not in os.environ:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29533", RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        _HOST_GROUP[0] = dist.new_group(backend="gloo")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    # MIOpen picks the fastest conv algorithm per shape during the warm-up
+    # steps (the image branch's NHWC convs: 14 -> 11 ms fwd+bwd)
+    torch.backends.cudnn.benchmark = True
+
+    import svdformer_pointsea_amd as pkg
+
+    pkg.lib()  # fail loudly if libpcops.so is missing
+    tuned = setup_tunableop(args.tunableop, args.model, rank)
+    wl = Workload(args.model)
+    if args.batch is None:
+        args.batch = wl.batch
+    amp = not args.fp32
+    leg = train_leg(args, wl, args.batch, amp, args.steps, args.warmup, device, world, rank, use_dist,
+                    not args.no_kernel_timing, "headline")
+    elapsed, spans, span_steps, sync = leg.elapsed, leg.spans, leg.span_steps, leg.sync
+    use_graph, host_ms, nparams = leg.use_graph, leg.host * 1e3 / args.steps, leg.nparams
 
     fp32_leg = None
+    extra = {}
     if args.model == "svdformer" and not args.fp32 and not args.no_fp32_leg:
         progress("configs[1] leg: fp32 forward + get_loss, B=16")
-        fp32_leg = fp32_forward_loss(wl, model, partial, gt, device, steps=max(3, args.steps // 2),
+        fp32_leg = fp32_forward_loss(wl, leg.model, leg.partial, leg.gt, device, steps=max(3, args.steps // 2),
                                      use_graph=use_graph)
     rows = kernel_table(spans)
+    if world == 1 and not args.no_extra_legs and args.model == "svdformer" and not args.fp32:
+        del leg
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        leg_steps = max(3, args.steps // 2)
+        # the reference's own arithmetic (fp32, core/train_pcn.py:101-134 has no AMP) at the headline shape
+        extra["fp32_train_step"] = extra_leg(args, "svdformer", args.batch, False, device, leg_steps)
+        # configs[4]: the ShapeNet-55 PointSea step (core/train_55.py:141-181), one GPU's B = 16
+        extra["pointsea_train_step"] = extra_leg(args, "pointsea", 16, True, device, leg_steps)
     out = None
     if rank == 0:
         samples = args.batch * world * args.steps
@@ -740,13 +831,12 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
-            "host_issue_ms_per_step": host * 1e3 / args.steps,
+            "host_issue_ms_per_step": host_ms,
             "execution": "hip_graph" if use_graph else "eager",
-            "kernel_timing_nonfinite": timing_nonfinite,
             "grad_sync": ("none (single GPU)" if not use_dist else
-                          f"bucketed all-reduce from backward hooks ({len(sync[0].buckets)} buckets of "
+                          f"bucketed all-reduce from backward hooks ({len(sync.buckets)} buckets of "
                           f"<= {args.bucket_mb:g} MB){' inside the captured graph' if use_graph else ''}"
-                          if sync[0] is not None else "one all-reduce of the flat bucket after backward"),
+                          if sync is not None else "one all-reduce of the flat bucket after backward"),
             "gemm_selection": (f"TunableOp ({args.tunableop}): {os.path.relpath(tuned, ROOT)}" if tuned
                                else "hipBLASLt heuristics"),
             "kernel_timing": ("HIP events per libpcops launch, %d eager steps after the timed graph replays"
@@ -785,6 +875,7 @@ def main():
                 out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) /
                                                          sum(r["ms"] for r in group), 4)
             step_ms = elapsed * 1e3 / args.steps
+
             def pmc_row(k, r):
                 t = pmc_traffic(args.pmc_json, k, r["name"])
                 if t is None or not r.get("work") or r.get("unit") != "GB/s":
@@ -799,6 +890,7 @@ def main():
                               for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
         if fp32_leg is not None:
             out["fp32_forward_loss"] = fp32_leg
+        out.update(extra)
         if world == 1 and not args.no_cpu_baseline:
             progress(f"timed {out['ms_per_step']:.2f} ms/step; CPU baseline")
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_steps)

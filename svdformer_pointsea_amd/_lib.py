@@ -238,23 +238,38 @@ def side_stream(device, lane=0):
 
 
 class fork:
-    """`with fork(device) as s:` runs the block on the side stream after the
-    current stream's pending work; `join(*tensors)` makes the current stream
-    wait for it and marks the tensors as used there.  No-op on CPU tensors."""
+    """`with fork(device, inputs=(x, ...)) as s:` runs the block on the side
+    stream after the current stream's pending work; `join(*tensors)` makes the
+    current stream wait for it and marks the tensors as used there.  No-op on
+    CPU tensors.
+
+    Memory safety across the two streams (the caching allocator only knows the
+    stream a block was allocated on):
+      * `inputs` -- every tensor the block reads that was allocated on the
+        current stream -- are recorded on the side stream at entry.  The block's
+        autograd nodes differentiate on the side stream too, and the saved
+        tensors they read there may be released on the host before those
+        kernels run; without the record the next current-stream allocation can
+        take the block while a side-stream forward or backward kernel still
+        reads it.
+      * the block's outputs are recorded on the current stream by `join`."""
 
     # PCOPS_SIDE_STREAMS=0 runs every block on the current stream (A/B runs, and
     # the only safe way to put hipBLASLt GEMMs inside a forked block)
     enabled = os.environ.get("PCOPS_SIDE_STREAMS", "1") != "0"
 
-    def __init__(self, device, lane=0):
+    def __init__(self, device, lane=0, inputs=()):
         self.on = fork.enabled and torch.device(device).type == "cuda"
         if self.on:
             self.main = torch.cuda.current_stream(device)
             self.side = side_stream(device, lane)
+            self.inputs = tuple(t for t in inputs if isinstance(t, torch.Tensor) and t.is_cuda)
 
     def __enter__(self):
         if self.on:
             self.side.wait_stream(self.main)
+            for t in self.inputs:
+                t.record_stream(self.side)
             self._ctx = torch.cuda.stream(self.side)
             self._ctx.__enter__()
             _TLS.side = getattr(_TLS, "side", 0) + 1

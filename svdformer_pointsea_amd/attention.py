@@ -115,12 +115,39 @@ class _Linear(Function):
         if ctx.has_b and ctx.needs_input_grad[2]:
             # a LayerNorm backward that consumed this output may have summed g
             # already (pcops_layernorm_bwd_colsum, attached to g); else one colsum
-            pre = getattr(g, _PRESUM, None)
+            pre = _take_sum(g)
             gb = pre if pre is not None else colsum(g2.contiguous())
         return gx, gw, gb
 
 
 _PRESUM = "_pcops_bias_colsum"   # attribute a gradient tensor carries when its column sum is known
+
+
+def _attach_sum(g, dsum):
+    """Hand the column sum of gradient `g` (computed by the launch that wrote g)
+    to the _Linear backward that consumes g, as (sum, producing stream)."""
+    setattr(g, _PRESUM, (dsum, torch.cuda.current_stream(g.device)))
+
+
+def _take_sum(g):
+    """The column sum attached to `g`, made safe on the consuming stream, or None.
+
+    The sum reaches the consumer outside autograd, so autograd's cross-stream
+    ordering and allocator bookkeeping do not cover it: the consumer waits for
+    the producing stream when it differs (it is the same stream in every path
+    the blocks issue today), records the sum on its own stream so the
+    allocator keeps the block until the consumer's kernels have run, and
+    detaches it from g (taken exactly once)."""
+    ent = getattr(g, _PRESUM, None)
+    if ent is None:
+        return None
+    delattr(g, _PRESUM)
+    dsum, producer = ent
+    cur = torch.cuda.current_stream(g.device)
+    if producer != cur:
+        cur.wait_stream(producer)
+    dsum.record_stream(cur)
+    return dsum
 
 
 class _nullctx:
@@ -433,7 +460,7 @@ class _LayerNorm(Function):
             # a and b may share one gradient tensor: the sum goes on a view
             # of its own, so only the summed input's producer sees it
             g = ga.view_as(ga) if ctx.sum_of == 0 else gb.view_as(gb)
-            setattr(g, _PRESUM, dsum)
+            _attach_sum(g, dsum)
             if ctx.sum_of == 0:
                 ga = g
             else:
@@ -454,10 +481,9 @@ def layer_norm(norm, a, b=None, sum_of=None):
 
 def _from_linear(t):
     """t is the output of a biased _Linear whose bias needs a gradient, issued
-    on the main stream.  Inside side-stream blocks the separate colsum stays:
-    there the pre-summed tensor crossed streams between its producer and the
-    Linear's backward and the captured step produced non-finite losses
-    (measured; the fused sums are a main-stream optimisation only)."""
+    on the main stream.  Inside side-stream blocks the separate colsum stays
+    (PCOPS_FUSED_SIDE=1 lifts that for A/B runs): the fused sums were measured
+    as a main-stream optimisation only."""
     fn = t.grad_fn if t is not None else None
     return (fn is not None and type(fn).__name__ == "_LinearBackward" and _FUSED_BIAS_SUM
             and (_FUSED_SIDE or not _lib.on_side_stream()))
@@ -488,7 +514,7 @@ class _Gelu(Function):
             call("gelu_bwd", lib().pcops_gelu_bwd_colsum, ptr(g), ptr(u), _dt(u), rows, C, ptr(du), ptr(dsum),
                  ptr(ws), wsb, stream_of(u))
         if dsum is not None:
-            setattr(du, _PRESUM, dsum)
+            _attach_sum(du, dsum)
         return du, None
 
 
@@ -578,10 +604,8 @@ _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switc
 _WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switch: split-K weight gradients
 _PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
 _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnostic: fused sums in side-stream blocks too
-# linear11's bias sum inside the GELU backward: off by default -- 2 of 4 bench
-# runs with it on ended with a non-finite loss in the timed steps, cause not
-# found (identical-input gradients match the separate colsum to bf16 noise,
-# and 50 graph replays without the optimizer stayed finite)
+# linear11's bias sum inside the GELU backward (A/B switch); the sum reaches the
+# Linear's backward through _attach_sum / _take_sum (stream-safe hand-off)
 _GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
 
 

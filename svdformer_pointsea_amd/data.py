@@ -78,8 +78,9 @@ def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=
             input_data = _pack(xyz, order, num_crop, n - num_crop, n - int(crop[0]))
         crop_data = _pack(xyz, order, torch.zeros_like(num_crop), num_crop, hi)
         # the two FPS launches (B workgroups each) run side by side
-        with fork(dev) as br:
-            crop_out = fps_subsample(crop_data.contiguous(), 2048)
+        crop_data = crop_data.contiguous()
+        with fork(dev, inputs=(crop_data,)) as br:
+            crop_out = fps_subsample(crop_data, 2048)
         input_out = fps_subsample(input_data.contiguous(), 2048)
         return input_out, br.join(crop_out)
     k = int(crop)

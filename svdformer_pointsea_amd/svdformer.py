@@ -575,7 +575,7 @@ class Model(nn.Module):
         # the local encoder (EdgeConv kNN, FPS, 1x1-conv GEMMs on rocBLAS: no stream-K)
         # only depends on the partial cloud: it runs on a second HIP stream
         # beside the view/point encoder
-        with fork(partial.device) as br:
+        with fork(partial.device, inputs=(partial_cm,)) as br:
             local_feat = self.localencoder(partial_cm)
         feat_g, coarse = self.encoder(partial_cm, depth)
         local_feat = br.join(local_feat)

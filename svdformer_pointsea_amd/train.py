@@ -170,14 +170,18 @@ class FlatParams:
             self.grad[:self.n16].copy_(self.grad16)
             self._collect32(self.n16, self.n_train, self._order32)
 
-    def _collect32(self, lo, hi, entries):
+    def _collect32(self, lo, hi, entries, stream=None):
         """bucket[lo:hi] <- the fp32 gradients autograd produced for `entries` (flat order),
-        zeros where none arrived; .grad points at the bucket again afterwards."""
+        zeros where none arrived; .grad points at the bucket again afterwards.
+        `stream`: the stream the gather runs on when it is not the one the
+        gradients were produced on (they are recorded there before .grad lets go)."""
         if not self._own32 or not entries:
             return
         parts = []
         for p, view in entries:
             g = p.grad
+            if g is not None and stream is not None:
+                g.record_stream(stream)
             parts.append(self._zeros32[:p.numel()] if g is None else self._physical(g, p))
         torch.cat(parts, out=self.grad[lo:hi])
         for p, view in entries:
@@ -284,18 +288,26 @@ class BucketedAllReduce:
 
     def _reduce(self, lo, hi, es):
         fp = self.fp
+        # the gradients were produced on the compute stream(s) and are read here on
+        # the communication stream: each is recorded on it, so the allocator cannot
+        # hand its block to the rest of backward before the gather below has run
+        comm = self.comm if self.on_gpu else None
         with torch.no_grad():
             if es[0][3]:   # bf16 shadows: their gradients into the flat bf16 then the fp32 bucket
-                parts = []
-                for o, n, w, _ in sorted(es, key=lambda e: e[0]):
-                    g = w.grad
-                    parts.append(torch.zeros(n, dtype=fp.grad16.dtype, device=fp.grad16.device)
-                                 if g is None else fp._physical(g, w))
-                torch.cat(parts, out=fp.grad16[lo:hi])
+                if _GRADS != "preset":   # preset: the gradients already live in grad16[lo:hi]
+                    parts = []
+                    for o, n, w, _ in sorted(es, key=lambda e: e[0]):
+                        g = w.grad
+                        if g is not None and comm is not None:
+                            g.record_stream(comm)
+                        parts.append(torch.zeros(n, dtype=fp.grad16.dtype, device=fp.grad16.device)
+                                     if g is None else fp._physical(g, w))
+                    torch.cat(parts, out=fp.grad16[lo:hi])
                 fp.grad[lo:hi].copy_(fp.grad16[lo:hi])
             elif fp._own32:   # fp32 parameters: autograd-owned gradients into the bucket
                 view = {id(p): v for p, v in fp._order32}
-                fp._collect32(lo, hi, [(w, view[id(w)]) for o, n, w, _ in sorted(es, key=lambda e: e[0])])
+                fp._collect32(lo, hi, [(w, view[id(w)]) for o, n, w, _ in sorted(es, key=lambda e: e[0])],
+                              stream=comm)
             seg = fp.grad[lo:hi]
             self.dist.all_reduce(seg, group=self.group)
             seg.mul_(1.0 / self.world)
@@ -407,13 +419,29 @@ def checkpoint_state(model, optimizer, fp=None, prefix="module."):
         for k, v in flat_state.items():
             if torch.is_tensor(v) and v.numel() == fp.n_train:
                 ent[k] = v[o:o + p.numel()].view_as(p).clone()
+            elif k == "step" and torch.is_tensor(v):
+                # the per-tensor optimizer keeps its step as a host fp32 scalar
+                ent[k] = v.detach().to("cpu", torch.float32).clone()
             else:
                 ent[k] = v.clone() if torch.is_tensor(v) else v
         state[i] = ent
     (group,) = osd["param_groups"]
+    return {"model": sd, "optimizer": {"state": state, "param_groups": [_reference_group(group, len(names))]}}
+
+
+def _reference_group(group, nparams):
+    """The flat optimizer's param_group as the reference's per-tensor Adam/AdamW
+    writes it (core/train_pcn.py:57-60, core/train_55.py:86-88): host-float
+    learning rates and the constructor defaults for the implementation
+    switches the bench turns on (fused / capturable / foreach), so loading the
+    checkpoint into torch.optim.Adam(model.parameters()) inherits none of them."""
     group = dict(group)
-    group["params"] = list(range(len(names)))
-    return {"model": sd, "optimizer": {"state": state, "param_groups": [group]}}
+    for k in ("lr", "initial_lr"):
+        if torch.is_tensor(group.get(k)):
+            group[k] = float(group[k])
+    group["fused"], group["capturable"], group["foreach"] = None, False, None
+    group["params"] = list(range(nparams))
+    return group
 
 
 def load_checkpoint_state(ckpt, model, optimizer, fp=None, prefix="module."):

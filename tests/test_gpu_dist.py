@@ -43,16 +43,23 @@ class _Net(nn.Module):
         self.head = nn.Linear(64, 3)
         self.side = nn.Linear(32, 48)
         self.unused = nn.Linear(5, 5)
+        # fp32 (LayerNorm) parameters after the head: with tiny buckets they form
+        # several fp32 buckets gathered on the communication stream while the
+        # rest of backward still allocates on the compute stream
+        self.post = nn.ModuleList(nn.LayerNorm(3) for _ in range(3))
 
     def forward(self, x):
         from svdformer_pointsea_amd import _lib
 
         # a branch on a side stream (as the model's local encoder): its weight
         # gradients are produced on that stream during backward
-        with _lib.fork(x.device, lane=3) as br:
+        with _lib.fork(x.device, lane=3, inputs=(x,)) as br:
             z = self.side(x.mean(2))
         y = self.blk(x).transpose(1, 2)
-        return self.head(self.norm(y.float())).float().square().mean() + br.join(z).float().square().mean()
+        h = self.head(self.norm(y.float())).float()
+        for m in self.post:
+            h = m(h) * 1.5 + h
+        return h.square().mean() + br.join(z).float().square().mean()
 
 
 def _step(fp, x, sync):
@@ -69,8 +76,8 @@ def _step(fp, x, sync):
     return loss.detach()
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_bucketed_allreduce_rccl(dev, group, graph):
+@pytest.mark.parametrize("graph,bucket_mb", [(False, 0.01), (True, 0.01), (False, 1e-5), (True, 1e-5)])
+def test_bucketed_allreduce_rccl(dev, group, graph, bucket_mb):
     from svdformer_pointsea_amd.train import BucketedAllReduce, FlatParams
 
     torch.manual_seed(0)
@@ -80,8 +87,10 @@ def test_bucketed_allreduce_rccl(dev, group, graph):
     fa, fb = FlatParams(a, dev), FlatParams(b, dev)
     _step(fa, x, None)
     ref = fa.grad.clone()
-    sync = BucketedAllReduce(fb, 1, bucket_mb=0.01)
+    sync = BucketedAllReduce(fb, 1, bucket_mb=bucket_mb)
     assert len(sync.buckets) > 4
+    if bucket_mb < 1e-4:   # every parameter its own bucket: several fp32 buckets
+        assert sum(1 for _, _, es in sync.buckets if not es[0][3]) >= 4
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):

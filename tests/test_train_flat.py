@@ -218,3 +218,44 @@ def test_checkpoint_interop_with_per_tensor_optimizer():
     train(lambda x: sb(x, fc, oc), 2, 10)
     for (n, pa), (_, pc) in zip(a.named_parameters(), c.named_parameters()):
         assert torch.equal(pa.data, pc.data), n
+
+
+def test_checkpoint_from_capturable_tensor_lr_optimizer_loads_into_plain_adam():
+    """bench.py's optimizer is capturable with a tensor LR (a captured graph reads it);
+    its checkpoint must still be the reference's: host-float lr, default fused /
+    capturable / foreach, host step -- a plain per-tensor Adam loads it and then
+    steps exactly like the optimizer that wrote it."""
+    from svdformer_pointsea_amd.train import checkpoint_state
+
+    torch.manual_seed(6)
+    a = _Net3()
+    b = copy.deepcopy(a)
+    fb = FlatParams(b, "cpu", bf16=False)
+    ob = torch.optim.Adam([fb.master()], lr=torch.tensor(1e-2), foreach=False)
+    oa = torch.optim.Adam(a.parameters(), lr=1e-2)
+    for step in range(2):
+        x = torch.randn(2, 4, 3, 5, generator=torch.Generator().manual_seed(step))
+        fb.zero_grad()
+        fb.forward(x).backward()
+        ob.step()
+        oa.zero_grad(set_to_none=True)
+        a(x).backward()
+        oa.step()
+    # the group flags bench.py's CUDA optimizer carries (capturable / fused need a GPU here)
+    ob.param_groups[0].update(capturable=True, fused=True)
+    ck = checkpoint_state(b, ob, fb)
+    (g,) = ck["optimizer"]["param_groups"]
+    assert isinstance(g["lr"], float) and g["capturable"] is False and g["fused"] is None and g["foreach"] is None
+    assert all(not ent["step"].is_cuda and ent["step"].dtype == torch.float32 for ent in ck["optimizer"]["state"].values())
+    c = _Net3()
+    c.load_state_dict({k[len("module."):]: v for k, v in ck["model"].items()})
+    oc = torch.optim.Adam(c.parameters(), lr=1e-2)
+    oc.load_state_dict(ck["optimizer"])
+    assert oc.param_groups[0]["capturable"] is False
+    x = torch.randn(2, 4, 3, 5, generator=torch.Generator().manual_seed(9))
+    for opt, m in ((oa, a), (oc, c)):
+        opt.zero_grad(set_to_none=True)
+        m(x).backward()
+        opt.step()
+    for (n, pa), (_, pc) in zip(a.named_parameters(), c.named_parameters()):
+        torch.testing.assert_close(pc.data, pa.data, rtol=1e-6, atol=1e-7, msg=n)
