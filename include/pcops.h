@@ -83,6 +83,19 @@ int pcops_sa_group(const float *xyz, const float *new_xyz, const float *points_t
 int pcops_sa_group_grad(const void *grad_out, int grad_dtype, const int *idx, int B, int N, int S, int K, int C,
                         float *grad_points_t, pcops_stream_t stream);
 
+/* EdgeConv edge features (models/model_utils.py:847-881, models_PointSea/model_utils.py:551-585):
+ * group_local's neighbour gather (:812-845), `central - neigh`, torch.cat((edge, central), 1) and
+ * the channels_last copy of the first 1x1 conv's input in one pass.  x (B,N,C) token-major fp32,
+ * idx (B,N,K) int32 (the feature-space kNN) -> out (B,N,K,2C) row-major:
+ *   out[b,n,k,c] = x[b,n,c] - x[b,idx,c],  out[b,n,k,C+c] = x[b,n,c]
+ * out_dtype 0 = fp32, 1 = bf16 (the difference rounded once). */
+int pcops_edge_group(const float *x, const int *idx, int B, int N, int K, int C, void *out, int out_dtype,
+                     pcops_stream_t stream);
+/* grad_x (B,N,C) fp32, overwritten: sum_k (g[b,n,k,c] + g[b,n,k,C+c]) minus the scatter of
+ * g[..., :C] by idx (index_points' backward).  grad_dtype 0 = fp32, 1 = bf16. */
+int pcops_edge_group_grad(const void *grad_out, int grad_dtype, const int *idx, int B, int N, int K, int C,
+                          float *grad_x, pcops_stream_t stream);
+
 /* pcops_max_k: torch.max(x, dim=3) of a (B, C, S, K) conv output held channels_last, i.e. over
  *   the middle dim of a contiguous (rows = B*S, K, C) tensor (models/model_utils.py:354, 862-864):
  *   out[r][c] = max_k x[r][k][c], arg[r][c] = the first maximising k (NaN is the maximum, as

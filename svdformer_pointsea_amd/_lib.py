@@ -53,6 +53,8 @@ _SIGS = {
     "pcops_attention_bwd_dq_delta": (I, [P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
     "pcops_transpose_add": (I, [P, I, P, I, P, I, P, I, I, I, I, P]),
     "pcops_add": (I, [P, I, P, I, P, I, LL, P]),
+    "pcops_edge_group": (I, [P, P, I, I, I, I, P, I, P]),
+    "pcops_edge_group_grad": (I, [P, I, P, I, I, I, I, P, P]),
     "pcops_max_k": (I, [P, I, LL, I, I, P, P, P]),
     "pcops_max_k_grad": (I, [P, I, P, LL, I, I, P, P]),
     "pcops_gelu_bwd_colsum": (I, [P, P, I, LL, I, P, P, P, ULL, P]),

@@ -388,6 +388,115 @@ __global__ __launch_bounds__(256) void max_k_grad_kernel(const void *__restrict_
   }
 }
 
+// ---- EdgeConv edge features (models/model_utils.py:847-881; PointSea's copy
+// models_PointSea/model_utils.py:551-585): group_local's kNN gather (:812-845),
+// `central - neigh`, torch.cat((edge, central), 1) and the channels_last copy the
+// first 1x1 conv reads, as ONE pass after the kNN:
+//   out[b,n,k,c]     = x[b,n,c] - x[b,idx[b,n,k],c]    (c < C)
+//   out[b,n,k,C + c] = x[b,n,c]
+// x (B,N,C) token-major fp32 -- the kNN's own operand -- so a neighbour is one
+// contiguous row (the reference's channel-major gather reads C strided floats
+// per neighbour).  Differences in fp32, rounded once to out's dtype (the
+// autocast cast the first conv would apply).  V = 8: C % 8 == 0, a thread
+// writes 8 channels (16-B bf16 / 32-B fp32 stores); V = 1 otherwise (C = 3).
+template <int V, int DT>
+__global__ __launch_bounds__(256) void edge_group_kernel(const float *__restrict__ x, const int *__restrict__ idx,
+                                                         int N, int K, int C, long long rows,
+                                                         void *__restrict__ out) {
+  const int cv = C / V, per = 2 * cv;  // vector chunks per output row
+  const long long total = rows * per;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long row = e / per;           // (b, n, k)
+    const int j = (int)(e - row * per);
+    const long long bn = row / K;            // (b, n)
+    const long long b = bn / N;
+    const bool edge = j < cv;
+    const int c = (edge ? j : j - cv) * V;
+    const float *xi = x + bn * C + c;
+    float v[V];
+#pragma unroll
+    for (int t = 0; t < V; ++t) v[t] = xi[t];
+    if (edge) {
+      const int a = idx[row];
+      if ((unsigned)a < (unsigned)N) {
+        const float *xj = x + (b * N + a) * C + c;
+#pragma unroll
+        for (int t = 0; t < V; ++t) v[t] -= xj[t];
+      }
+    }
+    const long long o = row * 2 * C + (edge ? c : C + c);
+    if constexpr (V == 8) {
+      Vec8<DT>::st(out, o, v);
+    } else if constexpr (DT == 1) {
+      reinterpret_cast<__bf16 *>(out)[o] = (__bf16)v[0];
+    } else {
+      reinterpret_cast<float *>(out)[o] = v[0];
+    }
+  }
+}
+
+// Backward, own term: dx[b,n,c] = sum_k (g[b,n,k,c] + g[b,n,k,C+c])  (the gradient
+// through `central`, used by the subtraction and the concat; k ascending, fp32),
+// stored -- no zero fill, no atomics.
+template <int V, int DT>
+__global__ __launch_bounds__(256) void edge_group_grad_own_kernel(const void *__restrict__ g, int K, int C,
+                                                                  long long pts, float *__restrict__ dx) {
+  const int cv = C / V;
+  const long long total = pts * cv;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long bn = e / cv;
+    const int c = (int)(e - bn * cv) * V;
+    float acc[V], a[V], b2[V];
+#pragma unroll
+    for (int t = 0; t < V; ++t) acc[t] = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const long long r = (bn * K + k) * 2 * C;
+      if constexpr (V == 8) {
+        Vec8<DT>::ld(a, g, r + c);
+        Vec8<DT>::ld(b2, g, r + C + c);
+      } else {
+        a[0] = DT == 1 ? (float)reinterpret_cast<const __bf16 *>(g)[r + c] : reinterpret_cast<const float *>(g)[r + c];
+        b2[0] = DT == 1 ? (float)reinterpret_cast<const __bf16 *>(g)[r + C + c]
+                        : reinterpret_cast<const float *>(g)[r + C + c];
+      }
+#pragma unroll
+      for (int t = 0; t < V; ++t) acc[t] += a[t] + b2[t];
+    }
+    if constexpr (V == 8) {
+      Vec8<0>::st(dx, bn * C + c, acc);
+    } else {
+      dx[bn * C + c] = acc[0];
+    }
+  }
+}
+
+// Backward, neighbour term: dx[b,idx[b,n,k],c] -= g[b,n,k,c] (the index_points /
+// group_points_grad scatter, token-major: a thread's V atomics hit one row).
+template <int V, int DT>
+__global__ __launch_bounds__(256) void edge_group_grad_scatter_kernel(const void *__restrict__ g,
+                                                                      const int *__restrict__ idx, int N, int K, int C,
+                                                                      long long rows, float *__restrict__ dx) {
+  const int cv = C / V;
+  const long long total = rows * cv;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long row = e / cv;
+    const int c = (int)(e - row * cv) * V;
+    const int a = idx[row];
+    if ((unsigned)a >= (unsigned)N) continue;
+    const long long b = row / ((long long)N * K);
+    float v[V];
+    if constexpr (V == 8) {
+      Vec8<DT>::ld(v, g, row * 2 * C + c);
+    } else {
+      v[0] = DT == 1 ? (float)reinterpret_cast<const __bf16 *>(g)[row * 2 * C + c]
+                     : reinterpret_cast<const float *>(g)[row * 2 * C + c];
+    }
+    float *d = dx + (b * N + a) * C + c;
+#pragma unroll
+    for (int t = 0; t < V; ++t) atomicAdd(d + t, -v[t]);
+  }
+}
+
 unsigned grid_for_ll(long long total) {
   long long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
@@ -425,6 +534,66 @@ extern "C" int pcops_max_k_grad(const void *grad_out, int dtype, const unsigned 
   else
     hipLaunchKernelGGL(max_k_grad_kernel<1>, dim3(grid_for_ll(total)), dim3(256), 0, (hipStream_t)stream, grad_out,
                        arg, rows, K, C, grad_x);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+namespace {
+template <int V>
+void edge_group_go(const float *x, const int *idx, int N, int K, int C, long long rows, void *out, int dt,
+                   hipStream_t s) {
+  const unsigned grid = grid_for_ll(rows * 2 * (C / V));
+  if (dt == 1)
+    hipLaunchKernelGGL((edge_group_kernel<V, 1>), dim3(grid), dim3(256), 0, s, x, idx, N, K, C, rows, out);
+  else
+    hipLaunchKernelGGL((edge_group_kernel<V, 0>), dim3(grid), dim3(256), 0, s, x, idx, N, K, C, rows, out);
+}
+
+template <int V, int DT>
+void edge_group_grad_go(const void *g, const int *idx, int B, int N, int K, int C, float *dx, hipStream_t s) {
+  const long long pts = (long long)B * N, rows = pts * K;
+  hipLaunchKernelGGL((edge_group_grad_own_kernel<V, DT>), dim3(grid_for_ll(pts * (C / V))), dim3(256), 0, s, g, K, C,
+                     pts, dx);
+  hipLaunchKernelGGL((edge_group_grad_scatter_kernel<V, DT>), dim3(grid_for_ll(rows * (C / V))), dim3(256), 0, s, g,
+                     idx, N, K, C, rows, dx);
+}
+}  // namespace
+
+extern "C" int pcops_edge_group(const float *x, const int *idx, int B, int N, int K, int C, void *out, int out_dtype,
+                                pcops_stream_t stream) {
+  if (B < 0 || N < 0 || K < 0 || C < 0 || (out_dtype != 0 && out_dtype != 1)) return PCOPS_ERR_INVALID;
+  const long long rows = (long long)B * N * K;
+  if (rows == 0 || C == 0) return PCOPS_OK;
+  if (!x || !idx || !out) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (C % 8 == 0 && ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0))
+    edge_group_go<8>(x, idx, N, K, C, rows, out, out_dtype, s);
+  else
+    edge_group_go<1>(x, idx, N, K, C, rows, out, out_dtype, s);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_edge_group_grad(const void *grad_out, int grad_dtype, const int *idx, int B, int N, int K, int C,
+                                     float *grad_x, pcops_stream_t stream) {
+  if (B < 0 || N < 0 || K < 0 || C < 0 || (grad_dtype != 0 && grad_dtype != 1)) return PCOPS_ERR_INVALID;
+  if ((long long)B * N * C == 0) return PCOPS_OK;
+  if (!grad_x) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (K == 0) {
+    if (hipMemsetAsync(grad_x, 0, sizeof(float) * (size_t)B * N * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!grad_out || !idx) return PCOPS_ERR_INVALID;
+  const bool vec = C % 8 == 0 && (uintptr_t)grad_out % 16 == 0 && (uintptr_t)grad_x % 16 == 0;
+  if (vec && grad_dtype == 1)
+    edge_group_grad_go<8, 1>(grad_out, idx, B, N, K, C, grad_x, s);
+  else if (vec)
+    edge_group_grad_go<8, 0>(grad_out, idx, B, N, K, C, grad_x, s);
+  else if (grad_dtype == 1)
+    edge_group_grad_go<1, 1>(grad_out, idx, B, N, K, C, grad_x, s);
+  else
+    edge_group_grad_go<1, 0>(grad_out, idx, B, N, K, C, grad_x, s);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

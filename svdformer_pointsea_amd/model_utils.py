@@ -9,6 +9,7 @@ its model classes can import them unchanged:
   fps_subsample(pcd, n_points=2048)                     :489-499
   sample_and_group_knn(xyz, points, npoint, k, ...)     :323-356
   sample_and_group_knn_cl (fused grouping, channels_last) :323-356 + the first conv's layout
+  edge_features (EdgeConv's [x_i - x_j, x_i], channels_last) :812-845, 869-877
   self_attention / cross_attention / SDG_Decoder        :542-629
   self_attention_woinp / SDG_Decoder_PointSea           models_PointSea/model_utils.py:463-509
   PCViews                                               :1179-1234
@@ -139,3 +140,49 @@ def sample_and_group_knn(xyz, points, npoint, k, use_xyz=True, idx=None):
     else:
         new_points = grouped_xyz
     return new_xyz, new_points, idx, grouped_xyz
+
+
+class _EdgeGroup(torch.autograd.Function):
+    """pcops_edge_group: EdgeConv's (x_i - x_j, x_i) rows in channels_last order."""
+
+    @staticmethod
+    def forward(ctx, x_t, idx, out_dtype):
+        B, N, C = x_t.shape
+        K = idx.shape[2]
+        out = torch.empty(B, N, K, 2 * C, dtype=out_dtype, device=x_t.device)
+        with torch.cuda.device(x_t.device):
+            call("edge_group", lib().pcops_edge_group, ptr(x_t), ptr(idx), B, N, K, C, ptr(out),
+                 1 if out_dtype == torch.bfloat16 else 0, stream_of(x_t))
+        ctx.save_for_backward(idx)
+        ctx.dims = (B, N, K, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        B, N, K, C = ctx.dims
+        if not ctx.needs_input_grad[0]:
+            return None, None, None
+        g = g.contiguous()
+        gx = torch.empty(B, N, C, dtype=torch.float32, device=g.device)
+        with torch.cuda.device(g.device):
+            call("edge_group_grad", lib().pcops_edge_group_grad, ptr(g), 1 if g.dtype == torch.bfloat16 else 0,
+                 ptr(idx), B, N, K, C, ptr(gx), stream_of(g))
+        return gx, None, None
+
+
+def edge_features(x, k, out_dtype=None):
+    """EdgeConv's edge features (model_utils.py:869-877): for the k feature-space
+    nearest neighbours j of every point i (group_local, :812-826), the rows
+    [x_i - x_j, x_i] -> (B, 2C, N, k) in channels_last memory, out_dtype (x's dtype
+    by default; bf16 under autocast is what the first 1x1 conv would cast to).
+    x (B, C, N).  Two launches: the kNN on the token-major fp32 cloud, then ONE
+    pass (pcops_edge_group) that gathers, subtracts, concatenates and writes the
+    conv's input layout -- in place of the grouping launch, repeat, subtract, cat
+    and channels_last copy."""
+    B, C, N = x.shape
+    if out_dtype is None:
+        out_dtype = x.dtype
+    pts = x.float().transpose(1, 2).contiguous()   # (B, N, C) fp32: the kNN's operand and the gather source
+    idx = _knn(pts.detach(), pts.detach(), k)
+    return _EdgeGroup.apply(pts, idx, out_dtype).permute(0, 3, 1, 2)

@@ -21,7 +21,7 @@ from torch import nn
 
 from .attention import SDG_Decoder, block_sum, cross_attention, linear, self_attention, to_channels, to_tokens
 from .chamfer3D import chamfer_3DDist
-from .model_utils import fps_subsample, group_local, sample_and_group_knn, sample_and_group_knn_cl
+from .model_utils import edge_features, fps_subsample, group_local, sample_and_group_knn, sample_and_group_knn_cl
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act, run_sequential
 from .conv import conv3x3
@@ -90,6 +90,8 @@ import os as _os
 # PCOPS_SA_FUSED=0: the unfused sample_and_group_knn path (A/B runs, parity tests)
 _SA_FUSED = _os.environ.get("PCOPS_SA_FUSED", "1") != "0"
 _MAXK = _os.environ.get("PCOPS_MAXK", "1") != "0"   # A/B switch: pcops_max_k for the neighbourhood max
+# PCOPS_EDGE_FUSED=0: EdgeConv's unfused group_local -> repeat -> subtract -> cat path (A/B, parity tests)
+_EDGE_FUSED = _os.environ.get("PCOPS_EDGE_FUSED", "1") != "0"
 
 
 def max_over_neighbours_tokens(x):
@@ -316,6 +318,13 @@ class EdgeConv(nn.Module):
 
     def forward(self, inputs):
         B, C, N = inputs.shape
+        if _EDGE_FUSED and self.num_neigh is not None and inputs.is_cuda:
+            # kNN -> ONE launch writing [x_i - x_j, x_i] into the first conv's channels_last
+            # input (model_utils.edge_features), in the dtype that conv computes in
+            dt = torch.bfloat16 if torch.is_autocast_enabled("cuda") else inputs.dtype
+            feature = edge_features(inputs, self.num_neigh, dt)
+            feature = run_sequential(self.conv, feature, lambda t, m: conv1x1(t, m, "edge"))
+            return max_over_neighbours(feature)
         if self.num_neigh is not None:
             neigh = group_local(inputs.float(), k=self.num_neigh).contiguous().to(inputs.dtype)
             central = inputs.unsqueeze(dim=3).repeat(1, 1, 1, self.num_neigh)

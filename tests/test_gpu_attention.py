@@ -696,5 +696,6 @@ def test_gelu_backward_kernel(dev, dt, rows, C):
     (ref,) = torch.autograd.grad(torch.nn.functional.gelu(ur), ur, g)
     tol = dict(rtol=1e-5, atol=1e-6) if dt == torch.float32 else dict(rtol=1e-2, atol=1e-3)
     torch.testing.assert_close(du.float(), ref.float(), **tol)
-    dsum = getattr(du, A._PRESUM)
+    dsum = A._take_sum(du)
+    assert A._take_sum(du) is None   # handed over exactly once
     torch.testing.assert_close(dsum, du.float().sum(0), rtol=1e-4, atol=1e-3)
