@@ -14,8 +14,15 @@
 //                          a rigorous rounding margin and re-derives the winner
 //                          with the direct expression (see its comment).
 //
-// Backward: own-point terms with plain stores, partner terms with float
-// atomics (the reference uses atomics for both, chamfer3D.cu:155-174).
+// Backward (chamfer3D.cu:155-195: own and partner terms both by float
+// atomics, so its sums depend on arrival order): one launch in which every
+// point's gradient is written exactly once, by the workgroup owning that point
+// as a partner TARGET.  The workgroup scans the source cloud's NN indices, and
+// the partner terms of its targets are summed in 64-bit fixed point in LDS
+// (integer adds: exact and order-independent -> bitwise reproducible), then
+// combined with the target's own term.  Scattered float atomics (one lane per
+// 12-B row) ran at the ~0.08 TB/s one-row-per-lane atomic rate; the old
+// two-kernel atomic form stays behind PCOPS_CHAMFER_BWD=atomic for A/B runs.
 #include <cstdlib>
 
 #include "common.h"
@@ -339,6 +346,105 @@ __global__ void chamfer_grad_partner_kernel(const float *__restrict__ xyz1, cons
   }
 }
 
+// Deterministic backward.  Direction d = 0: sources = cloud 1 (NN idx1 into cloud 2),
+// targets = cloud 2; d = 1 the other way.  Block (part, d, b) owns targets [j0, j1) and writes
+//   grad_T[j] = own_T[j] - sum_{i : idx_S[i] = j} c_i,   c_i = 2 gd_S[i] (s_i - t_j)
+//   own_T[j]  = 2 gd_T[j] (t_j - s_{idx_T[j]})
+// (the reference's expressions, chamfer3D.cu:155-174).  Pass 1 finds the largest finite |c| of
+// the block's targets; the scale 2^sh makes every term and every possible sum (at most NA
+// terms) fit int64, and pass 2 adds round(c * 2^sh) with LDS 64-bit integer atomics: exact and
+// order-independent.  Error per sum <= NA * 2^-(sh+1) ~ max|c| * 2^-48, then one rounding to
+// fp32 (the reference's fp32 atomic sum errs by ~2^-24 of the sum of |c| and varies run to run).
+// Non-finite terms set per-component flags (+inf / -inf / NaN, atomicOr): the sum is then
+// +-inf or NaN from the flags alone, again whatever the order.
+constexpr int kGThreads = 512;
+constexpr int kGTargets = 2048;   // targets per block at most: 2048 x (3 x 8 + 4) B = 56 KB of LDS
+
+__global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int N, int M, const float *__restrict__ gd1,
+    const float *__restrict__ gd2, const int *__restrict__ idx1, const int *__restrict__ idx2, float *__restrict__ g1,
+    float *__restrict__ g2, int parts0, int parts1) {
+  __shared__ long long acc[kGTargets * 3];
+  __shared__ int flags[kGTargets];
+  __shared__ float red[kGThreads / 64];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const bool dir = (int)blockIdx.x >= parts0;
+  const int part = dir ? blockIdx.x - parts0 : blockIdx.x;
+  const int parts = dir ? parts1 : parts0;
+  const int NA = dir ? M : N, NT = dir ? N : M;
+  const float *S = (dir ? xyz2 : xyz1) + (size_t)b * NA * 3;
+  const float *T = (dir ? xyz1 : xyz2) + (size_t)b * NT * 3;
+  const float *gS = (dir ? gd2 : gd1) + (size_t)b * NA;
+  const int *iS = (dir ? idx2 : idx1) + (size_t)b * NA;
+  const float *gT = (dir ? gd1 : gd2) + (size_t)b * NT;
+  const int *iT = (dir ? idx1 : idx2) + (size_t)b * NT;
+  float *out = (dir ? g1 : g2) + (size_t)b * NT * 3;
+  const int R = (NT + parts - 1) / parts;
+  const int j0 = part * R, j1 = min(NT, j0 + R);
+  if (j0 >= j1) return;
+
+  // pass 1: the largest finite |partner term| of this block's targets
+  float mx = 0.f;
+  for (int i = tid; i < NA; i += kGThreads) {
+    const int j = iS[i];
+    if (j < j0 || j >= j1) continue;
+    const float g = gS[i] * 2.f;
+    const float *p = S + (size_t)i * 3, *q = T + (size_t)j * 3;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float c = fabsf(g * (p[k] - q[k]));
+      if (c <= 3.4028234e38f) mx = fmaxf(mx, c);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  for (int e = tid; e < (j1 - j0) * 3; e += kGThreads) acc[e] = 0;
+  for (int e = tid; e < j1 - j0; e += kGThreads) flags[e] = 0;
+  __syncthreads();
+  mx = red[0];
+#pragma unroll
+  for (int w = 1; w < kGThreads / 64; ++w) mx = fmaxf(mx, red[w]);
+  int e2 = 0;
+  (void)frexpf(mx, &e2);                                 // mx < 2^e2
+  const int lg = 32 - __builtin_clz((unsigned)NA | 1u);  // NA < 2^lg terms per sum at most
+  const int sh = mx > 0.f ? 62 - e2 - lg : 0;
+  // pass 2: fixed-point adds of the finite terms, flags for the others
+  for (int i = tid; i < NA; i += kGThreads) {
+    const int j = iS[i];
+    if (j < j0 || j >= j1) continue;
+    const float g = gS[i] * 2.f;
+    const float *p = S + (size_t)i * 3, *q = T + (size_t)j * 3;
+    const int jj = j - j0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float c = g * (p[k] - q[k]);
+      if (fabsf(c) <= 3.4028234e38f)
+        atomicAdd(reinterpret_cast<unsigned long long *>(acc + jj * 3 + k),
+                  (unsigned long long)__builtin_llrint(__builtin_ldexp((double)c, sh)));
+      else
+        atomicOr(flags + jj, 1 << (3 * k + (c != c ? 2 : (c > 0.f ? 0 : 1))));
+    }
+  }
+  __syncthreads();
+  // every target of the block: own term minus the partner sum, written once
+  for (int jj = tid; jj < j1 - j0; jj += kGThreads) {
+    const int j = j0 + jj;
+    const int a = iT[j];
+    const float g = gT[j] * 2.f;
+    const float *t = T + (size_t)j * 3, *s2 = S + (size_t)((unsigned)a < (unsigned)NA ? a : 0) * 3;
+    const int f = flags[jj];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float own = g * (t[k] - s2[k]);
+      const int fk = (f >> (3 * k)) & 7;
+      double sum = __builtin_ldexp((double)acc[jj * 3 + k], -sh);
+      if (fk) sum = (fk & 4) || fk == 3 ? (double)NAN : (fk == 1 ? (double)INFINITY : -(double)INFINITY);
+      out[(size_t)j * 3 + k] = (float)((double)own - sum);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B, int N, int M, float *dist1,
@@ -408,6 +514,24 @@ extern "C" int pcops_chamfer_backward(const float *xyz1, const float *xyz2, int 
   }
   if (!xyz1 || !xyz2 || !graddist1 || !graddist2 || !idx1 || !idx2 || !gradxyz1 || !gradxyz2)
     return PCOPS_ERR_INVALID;
+  static const bool atomic_form = [] {  // PCOPS_CHAMFER_BWD=atomic: the two-kernel float-atomic form (A/B)
+    const char *e = getenv("PCOPS_CHAMFER_BWD");
+    return e && e[0] == 'a';
+  }();
+  if (!atomic_form) {
+    // at least ceil(NT / kGTargets) target ranges per (batch, direction); more (down to 512
+    // targets each) while the grid is under 2 blocks per CU
+    auto parts_for = [&](int NT) {
+      int p = (NT + kGTargets - 1) / kGTargets;
+      while ((long)B * 2 * p < 512 && (NT + 2 * p - 1) / (2 * p) >= 512) p *= 2;
+      return p;
+    };
+    const int p0 = parts_for(M), p1 = parts_for(N);
+    hipLaunchKernelGGL(chamfer_grad_seg_kernel, dim3(p0 + p1, B), dim3(kGThreads), 0, s, xyz1, xyz2, N, M, graddist1,
+                       graddist2, idx1, idx2, gradxyz1, gradxyz2, p0, p1);
+    PC_CHECK_LAUNCH();
+    return PCOPS_OK;
+  }
   const size_t tot = (size_t)B * (N + M);
   unsigned grid = (unsigned)((tot + 255) / 256);
   if (grid > 4096) grid = 4096;

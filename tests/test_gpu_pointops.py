@@ -179,6 +179,69 @@ def test_chamfer_bitexact_and_backward(dev, B, N, M):
     np.testing.assert_allclose(bt.grad.cpu().numpy(), g2, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("case", ["loss16384", "hub", "tiled", "inf_grad"])
+def test_chamfer_backward_deterministic(dev, case):
+    """The one-launch backward (partner terms summed per target in 64-bit fixed point):
+    bitwise identical across runs, within fp32 rounding of the oracle's sequential sums
+    (chamfer3D.cu:155-195), at the loss's 16384 x 16384 shape, with every source mapped
+    to one target (a hub: the fixed-point range at its widest), exact ties, and
+    non-finite upstream gradients (fp32 fallback: inf / NaN as the oracle)."""
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    rng = np.random.default_rng(len(case))
+    if case == "loss16384":
+        a, b = [(rng.random((2, 16384, 3)) - 0.5).astype(np.float32) for _ in range(2)]
+    elif case == "hub":
+        a = (rng.random((2, 3000, 3)) - 0.5).astype(np.float32)
+        b = (rng.random((2, 2500, 3)) * 100 + 50).astype(np.float32)
+        b[:, 17] = 0.0                      # every point of a has b[17] as its nearest
+    elif case == "tiled":
+        a, b = _tiled(rng, 2, 300, 3000), _tiled(rng, 2, 200, 4100)
+    else:
+        a, b = [(rng.random((1, n, 3)) - 0.5).astype(np.float32) for n in (2100, 2300)]
+    w1 = rng.random(a.shape[:2]).astype(np.float32)
+    w2 = rng.random(b.shape[:2]).astype(np.float32)
+    if case == "inf_grad":
+        w1[0, 3] = np.inf
+        w2[0, 11] = np.nan
+    grads = []
+    for _ in range(2):
+        at, bt = T(a, dev).requires_grad_(True), T(b, dev).requires_grad_(True)
+        d1, d2, i1, i2 = chamfer_3DDist()(at, bt)
+        ((d1 * T(w1, dev)).sum() + (d2 * T(w2, dev)).sum()).backward()
+        grads.append((at.grad.cpu().numpy(), bt.grad.cpu().numpy()))
+    for x, y in zip(grads[0], grads[1]):
+        assert np.array_equal(x, y, equal_nan=True)
+    i1, i2 = i1.cpu().numpy(), i2.cpu().numpy()
+    g1, g2 = O.chamfer_backward(a, b, w1, w2, i1, i2)
+    r1, r2 = _chamfer_grad64(a, b, w1, w2, i1, i2)
+    for got, ora, ref in ((grads[0][0], g1, r1), (grads[0][1], g2, r2)):
+        fin = np.isfinite(ref)
+        assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(got[np.isinf(ref)], ref[np.isinf(ref)])
+        scale = np.abs(ref[fin]).max()
+        # the fp32 rounding of the exact sum (fixed-point partner sums), against float64 ...
+        np.testing.assert_allclose(got[fin], ref[fin], rtol=2.5e-7, atol=1e-9 * scale)
+        # ... and the oracle's sequential fp32 sums within their own rounding (not for the hub's 3000-term sum)
+        if case != "hub":
+            np.testing.assert_allclose(got[fin], ora[fin], rtol=1e-5, atol=1e-6 * scale)
+
+
+def _chamfer_grad64(a, b, w1, w2, i1, i2):
+    """Float64 sums of the fp32 terms of chamfer3D.cu:155-174 (own + partners)."""
+    out = []
+    for S, T, gS, gT, iS, iT in ((b, a, w2, w1, i2, i1), (a, b, w1, w2, i1, i2)):
+        # targets = cloud T; own term from T's NN in S, partner terms from S's NN in T
+        B = T.shape[0]
+        own = (2 * gT[..., None]).astype(np.float32) * (T - np.take_along_axis(S, iT[..., None].astype(np.int64), 1))
+        c = (2 * gS[..., None]).astype(np.float32) * (S - np.take_along_axis(T, iS[..., None].astype(np.int64), 1))
+        with np.errstate(invalid="ignore"):
+            part = np.zeros(T.shape, np.float64)
+            for bb in range(B):
+                np.add.at(part[bb], iS[bb].astype(np.int64), c[bb].astype(np.float64))
+            out.append(own.astype(np.float64) - part)
+    return out
+
+
 def _screen_clouds(kind, rng):
     if kind == "uniform":
         return [(rng.random((2, n, 3)) - 0.5).astype(np.float32) for n in (3000, 5000)]
