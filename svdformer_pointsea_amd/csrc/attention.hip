@@ -986,10 +986,40 @@ bool dkv_split() {  // PCOPS_DKV_SPLIT=0 keeps the one-pass dK/dV kernel for D =
   return v;
 }
 
+// one dK/dV launch of a given shape: NW waves per block, MODE (0 one pass, 3 one pass by
+// 32-query halves -- the same per-accumulator order as 0, half the live S / dP), OCC waves / SIMD
+template <int D, int NW, int MODE, int OCC>
+int launch_dkv2_cfg(const void *q, const void *k, const void *v, const void *dout, const float *lse,
+                    const float *delta, void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st,
+                    hipStream_t s) {
+  using C = Fwd2Cfg<D, NW>;
+  const size_t lds = C::kLds + 4 * kKT * sizeof(float);
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW, MODE, OCC>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
+  const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
+  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, MODE, OCC>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
+                     (__bf16 *)dv, Lq, Lk, scale, st);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
 template <int D, int NW>
 int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                 void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
+  if constexpr (D == 64 && NW == 8) {
+    // occupancy variants of the long-sequence D = 64 pass (A/B: PCOPS_DKV64)
+    static const int var = env_int("PCOPS_DKV64", 0);
+    switch (var) {
+      case 1: return launch_dkv2_cfg<64, 4, 3, 2>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      case 2: return launch_dkv2_cfg<64, 4, 3, 3>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      case 3: return launch_dkv2_cfg<64, 8, 3, 2>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      case 4: return launch_dkv2_cfg<64, 4, 0, 2>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      default: break;
+    }
+  }
   const size_t lds = C::kLds + 4 * kKT * sizeof(float);
   const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
   if (D >= 96 && dkv_split()) {
@@ -1037,9 +1067,11 @@ int dq2_dispatch(const void *q, const void *k, const void *v, const void *dout, 
     }
     case 96:
       return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
-    case 128:
-      return wide ? launch_dq2<128, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
-                  : launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+    case 128: {
+      static const int nw4 = env_int("PCOPS_DQ128_NW4", 0);   // A/B: 4-wave key-half blocks at any length
+      return (wide && !nw4) ? launch_dq2<128, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
+                            : launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+    }
     default:
       return PCOPS_ERR_UNSUPPORTED;
   }

@@ -216,6 +216,267 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
   FPS_STAMP_FLUSH
 }
 
+// ---- work-pruned FPS (2048 < N <= 16384) ---------------------------------
+// Same result as fps_reg_kernel, bit for bit, with most of each round's sweep
+// skipped.  The winner of a round depends only on the multiset of (running
+// distance, tie priority) pairs, so the points can sit anywhere: they are
+// bucketed by a 12-bit Morton cell of the cloud's box once (LDS counting sort;
+// the order inside a cell is arbitrary and irrelevant) and every lane holds
+// PPT spatially adjacent points plus their bounding box.  A round skips a lane
+// when the box's squared distance to the new centre, shrunk by a rounding
+// margin, exceeds the lane's largest running distance: then no point of the
+// lane can lower its running min (fl(d) >= exact d (1 - 5u) >= lb (1 - 11u)
+// for the reference's fp32 expression), so the skipped update would have
+// changed nothing.  Late rounds touch only the lanes around the new centre.
+// Ties: point k's priority is the reference LDS tree's order, P(k) =
+// bitrev_L(k mod T) * R + k div T (smaller wins), folded into the key
+//   hi = running distance bits (>= 0),  lo = (16383 - P) << 18 | wave << 14 | k
+// and the round's winner is the max 64-bit key over the cloud.
+constexpr int kPruneThreads = 1024;
+constexpr int kCellBits = 4;                       // per axis: 16^3 = 4096 Morton cells
+constexpr int kCells = 1 << (3 * kCellBits);
+
+__device__ __forceinline__ unsigned spread3(unsigned v) {  // 4 bits -> every third bit
+  return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
+}
+
+template <int PPT>
+__global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *__restrict__ xyz, int N, int M, int T,
+                                                                  int L, int R, int *__restrict__ idx) {
+  const int b = blockIdx.x;
+  const float *p = xyz + (size_t)b * N * 3;
+  int *out = idx + (size_t)b * M;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  __shared__ int cnt[kCells];
+  __shared__ unsigned short perm[kPruneThreads * PPT];
+  __shared__ float sred[6][16];
+  __shared__ int sscan[16];
+  __shared__ uint2 skey2[2][16];
+  __shared__ float4 sxyz2[2][16];
+
+  // (1) the cloud's box (fminf / fmaxf drop NaN coordinates)
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int k = t + i * kPruneThreads;
+    if (k < N) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const float v = p[3 * k + a];
+        mn[a] = fminf(mn[a], v);
+        mx[a] = fmaxf(mx[a], v);
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    mn[a] = wave_min_f32(mn[a]);
+    mx[a] = wave_max_f32(mx[a]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      sred[a][w] = mn[a];
+      sred[3 + a][w] = mx[a];
+    }
+  }
+  for (int c = t; c < kCells; c += kPruneThreads) cnt[c] = 0;
+  if (t < 32) {
+    skey2[t >> 4][t & 15] = make_uint2(0u, 0u);
+    sxyz2[t >> 4][t & 15] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  float org[3], scl[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float lo = sred[a][0], hi = sred[3 + a][0];
+    for (int ww = 1; ww < 16; ++ww) {
+      lo = fminf(lo, sred[a][ww]);
+      hi = fmaxf(hi, sred[3 + a][ww]);
+    }
+    const float ext = hi - lo;
+    org[a] = lo;
+    scl[a] = ext > 0.f && ext < INFINITY ? (float)(1 << kCellBits) / ext : 0.f;
+  }
+  // (2) Morton cell of every point and its slot inside the cell
+  int cell[PPT], pos[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int k = t + i * kPruneThreads;
+    cell[i] = 0;
+    pos[i] = 0;
+    if (k < N) {
+      unsigned q[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const float f = fminf(fmaxf((p[3 * k + a] - org[a]) * scl[a], 0.f), (float)((1 << kCellBits) - 1));
+        q[a] = (unsigned)f;  // NaN -> fmaxf -> 0
+      }
+      cell[i] = (int)(spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2));
+      pos[i] = atomicAdd(&cnt[cell[i]], 1);
+    }
+  }
+  __syncthreads();
+  // (3) exclusive scan of the cell counts (kCells / kPruneThreads per thread)
+  {
+    constexpr int CPT = kCells / kPruneThreads;
+    int v[CPT], sum = 0;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      v[c] = cnt[t * CPT + c];
+      sum += v[c];
+    }
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) sscan[w] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int ww = 0; ww < w; ++ww) base += sscan[ww];
+    int run = base + incl - sum;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      cnt[t * CPT + c] = run;
+      run += v[c];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int k = t + i * kPruneThreads;
+    if (k < N) perm[cnt[cell[i]] + pos[i]] = (unsigned short)k;
+  }
+  __syncthreads();
+
+  // (4) this lane's PPT points (sorted slots t*PPT ...), their keys and box
+  float px[PPT], py[PPT], pz[PPT], tmp[PPT];
+  unsigned lo[PPT];
+  float bx0 = INFINITY, by0 = INFINITY, bz0 = INFINITY, bx1 = -INFINITY, by1 = -INFINITY, bz1 = -INFINITY;
+  bool has = false;
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int s = t * PPT + i;
+    px[i] = py[i] = pz[i] = 0.f;
+    tmp[i] = -1.f;  // never competes
+    lo[i] = 0u;
+    if (s < N) {
+      const int k = perm[s];
+      px[i] = p[3 * k];
+      py[i] = p[3 * k + 1];
+      pz[i] = p[3 * k + 2];
+      const float mag = sqd3(px[i], py[i], pz[i]);
+      if (!((double)mag <= 1e-3)) {  // sampling_gpu.cu:100-101
+        tmp[i] = 1e10f;
+        const unsigned P = bitrev_bits((unsigned)k & (unsigned)(T - 1), L) * (unsigned)R + ((unsigned)k >> L);
+        lo[i] = ((16383u - P) << 18) | ((unsigned)w << 14) | (unsigned)k;
+        bx0 = fminf(bx0, px[i]), by0 = fminf(by0, py[i]), bz0 = fminf(bz0, pz[i]);
+        bx1 = fmaxf(bx1, px[i]), by1 = fmaxf(by1, py[i]), bz1 = fmaxf(bz1, pz[i]);
+        has = true;
+      }
+    }
+  }
+  // the lane's best (running distance, priority) and its coordinates
+  float lmax = -1.f, cx = 0.f, cy = 0.f, cz = 0.f;
+  int lhi = 0, llo = 0;
+  auto lane_best = [&]() {
+    float m = -1.f;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) m = fmaxf(m, tmp[i]);
+    unsigned l = 0u;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const bool take = tmp[i] == m && lo[i] > l;
+      l = take ? lo[i] : l;
+      cx = take ? px[i] : cx;
+      cy = take ? py[i] : cy;
+      cz = take ? pz[i] : cz;
+    }
+    lmax = m;
+    lhi = m >= 0.f ? __float_as_int(m) : 0;
+    llo = m >= 0.f ? (int)l : 0;
+  };
+  lane_best();
+  int whi = 0, wlo = 0;
+  float wcx = 0.f, wcy = 0.f, wcz = 0.f;
+  auto wave_best = [&]() {
+    whi = wave_max_i32(lhi);
+    wlo = wave_max_i32(lhi == whi ? llo : INT_MIN);
+    const int wl = (int)__builtin_ctzll(__ballot(lhi == whi && llo == wlo));
+    wcx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), wl));
+    wcy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), wl));
+    wcz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), wl));
+  };
+  wave_best();
+
+  const float x0 = p[0], y0 = p[1], z0 = p[2];
+  float ox = x0, oy = y0, oz = z0;
+  if (t == 0 && M > 0) out[0] = 0;
+  constexpr float kShrink = 1.f - 1.f / 262144.f;  // 2^-18 >> the 11u rounding margin
+  for (int j = 1; j < M; ++j) {
+    const int par = j & 1;
+    const float gx = fmaxf(fmaxf(bx0 - ox, ox - bx1), 0.f);
+    const float gy = fmaxf(fmaxf(by0 - oy, oy - by1), 0.f);
+    const float gz = fmaxf(fmaxf(bz0 - oz, oz - bz1), 0.f);
+    const float lb = gx * gx + gy * gy + gz * gz;
+    bool changed = false;
+    if (has && !(lb * kShrink > lmax)) {
+#pragma unroll
+      for (int i = 0; i < PPT; ++i) {
+        const float nt = fminf(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz), tmp[i]);
+        changed |= nt != tmp[i];
+        tmp[i] = nt;
+      }
+      if (changed) lane_best();
+    }
+    if (__any(changed)) wave_best();
+    if (lane == 0) {
+      skey2[par][w] = make_uint2((unsigned)whi, (unsigned)wlo);
+      sxyz2[par][w] = make_float4(wcx, wcy, wcz, 0.f);
+    }
+    lds_barrier();
+    // 64-bit max over the 16 wave slots in one DPP row (every wave, no second barrier)
+    const uint2 kv = skey2[par][lane & 15];
+    const float4 cv = sxyz2[par][lane & 15];
+    unsigned long long key = ((unsigned long long)kv.x << 32) | kv.y;
+#define FPS_DPP_MAX(CTRL)                                                                                   \
+  {                                                                                                        \
+    const unsigned hi2 = __builtin_amdgcn_update_dpp(0, (int)(key >> 32), CTRL, 0xF, 0xF, false);          \
+    const unsigned lo2 = __builtin_amdgcn_update_dpp(0, (int)(unsigned)key, CTRL, 0xF, 0xF, false);        \
+    const unsigned long long o = ((unsigned long long)hi2 << 32) | lo2;                                    \
+    key = o > key ? o : key;                                                                               \
+  }
+    FPS_DPP_MAX(0xB1)
+    FPS_DPP_MAX(0x4E)
+    FPS_DPP_MAX(0x141)
+    FPS_DPP_MAX(0x140)
+#undef FPS_DPP_MAX
+    const unsigned ghi = __builtin_amdgcn_readfirstlane((unsigned)(key >> 32));
+    const unsigned glo = __builtin_amdgcn_readfirstlane((unsigned)key);
+    int k = 0;
+    if (ghi != 0u || glo != 0u) {
+      const int gw = (int)((glo >> 14) & 15u);
+      k = (int)(glo & 0x3FFFu);
+      ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.x), gw));
+      oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.y), gw));
+      oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.z), gw));
+    } else {  // no valid point at all: the reference's dists_i[0] == 0
+      ox = x0, oy = y0, oz = z0;
+    }
+    if (t == 0) out[j] = k;
+  }
+}
+
+bool fps_prune() {  // PCOPS_FPS_PRUNE=0: the full-sweep kernels for every N (A/B runs)
+  static const bool v = [] {
+    const char *e = getenv("PCOPS_FPS_PRUNE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 struct __align__(16) FpsSlot {
   float d, x, y, z;
   int k;
@@ -304,9 +565,25 @@ __global__ __launch_bounds__(kFpsThreads) void fps_stream_kernel(const float *__
   }
 }
 
+// The output elements are cut into 8 contiguous ranges, one per XCD (workgroups
+// are dispatched to the XCDs round-robin: block % 8): each XCD then gathers from
+// the point rows of its own batches only, and a 64-B line of `points` is fetched
+// into one XCD's L2 instead of up to eight (PMC: 5.5x the algorithmic bytes with
+// the plain grid-stride order).  gridDim.x is a multiple of 8.
+__device__ __forceinline__ void xcd_span(size_t total, size_t &e, size_t &end, size_t &stride) {
+  const unsigned xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per = gridDim.x >> 3;
+  const size_t chunk = (total + 7) / 8;
+  const size_t begin = xcd * chunk;
+  end = begin + chunk < total ? begin + chunk : total;
+  e = begin + (size_t)slot * blockDim.x + threadIdx.x;
+  stride = (size_t)per * blockDim.x;
+}
+
 __global__ void gather_kernel(const float *__restrict__ points, const int *__restrict__ idx, int C, int N, int M,
                               size_t total, float *__restrict__ out) {
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+  size_t e, end, stride;
+  xcd_span(total, e, end, stride);
+  for (; e < end; e += stride) {
     const int m = (int)(e % M);
     const size_t bc = e / M;
     const size_t b = bc / C;
@@ -317,7 +594,9 @@ __global__ void gather_kernel(const float *__restrict__ points, const int *__res
 
 __global__ void gather_grad_kernel(const float *__restrict__ grad_out, const int *__restrict__ idx, int C, int N,
                                    int M, size_t total, float *__restrict__ grad_points) {
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+  size_t e, end, stride;
+  xcd_span(total, e, end, stride);
+  for (; e < end; e += stride) {
     const int m = (int)(e % M);
     const size_t bc = e / M;
     const size_t b = bc / C;
@@ -354,6 +633,10 @@ unsigned grid_for(size_t total, int block) {
   return (unsigned)(g < 1 ? 1 : g);
 }
 
+unsigned grid_xcd(size_t total, int block) {  // a multiple of 8 workgroups (xcd_span)
+  return (grid_for(total, block) + 7u) & ~7u;
+}
+
 }  // namespace
 
 extern "C" unsigned long long pcops_fps_workspace_bytes(int B, int N) {
@@ -372,6 +655,17 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
   const int nthreads = T < 64 ? 64 : T;
   const int ppt = (N + T - 1) / T;  // points per reference thread
   hipStream_t s = (hipStream_t)stream;
+  if (N > 2048 && N <= kPruneThreads * 16 && fps_prune()) {
+    const int R = (N + T - 1) / T;  // points per reference thread (P(k) = rev(k mod T) * R + k / T)
+    if (N <= kPruneThreads * 4)
+      hipLaunchKernelGGL(fps_prune_kernel<4>, dim3(B), dim3(kPruneThreads), 0, s, xyz, N, M, T, L, R, idx);
+    else if (N <= kPruneThreads * 8)
+      hipLaunchKernelGGL(fps_prune_kernel<8>, dim3(B), dim3(kPruneThreads), 0, s, xyz, N, M, T, L, R, idx);
+    else
+      hipLaunchKernelGGL(fps_prune_kernel<16>, dim3(B), dim3(kPruneThreads), 0, s, xyz, N, M, T, L, R, idx);
+    PC_CHECK_LAUNCH();
+    return PCOPS_OK;
+  }
   if (ppt <= kFpsMaxPPT) {
     // clouds with > 16 points per reference thread use 2 hardware threads per
     // reference thread (1024 threads, 4 waves / SIMD).  Up to 16 the 8-wave
@@ -410,7 +704,7 @@ extern "C" int pcops_gather_points(const float *points, const int *idx, int B, i
   const size_t total = (size_t)B * C * M;
   if (total == 0) return PCOPS_OK;
   if (!points || !idx || !out) return PCOPS_ERR_INVALID;
-  hipLaunchKernelGGL(gather_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, points, idx, C,
+  hipLaunchKernelGGL(gather_kernel, dim3(grid_xcd(total, 256)), dim3(256), 0, (hipStream_t)stream, points, idx, C,
                      N, M, total, out);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
@@ -426,7 +720,7 @@ extern "C" int pcops_gather_points_grad(const float *grad_out, const int *idx, i
   const size_t total = (size_t)B * C * M;
   if (total == 0) return PCOPS_OK;
   if (!grad_out || !idx) return PCOPS_ERR_INVALID;
-  hipLaunchKernelGGL(gather_grad_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, grad_out, idx,
+  hipLaunchKernelGGL(gather_grad_kernel, dim3(grid_xcd(total, 256)), dim3(256), 0, (hipStream_t)stream, grad_out, idx,
                      C, N, M, total, grad_points);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;

@@ -23,6 +23,8 @@ SHAPES = [  # (B, H, Lq, Lk, E)
     (2, 2, 70, 130, 64),    # hd 32
     (2, 8, 2048, 2048, 512),   # refine2 self-attention at its real length (hd 64, 32 key tiles)
     (2, 8, 2048, 2048, 1024),  # refine2 decoder sa2 at its real length (hd 128)
+    (2, 8, 1024, 1024, 768),   # PointSea ShapeNet-55 refine1 (hd 96 at L = 1024, models_PointSea/model_utils.py:385-509)
+    (3, 4, 49, 49, 512),       # PointSea viewattn1: 7x7 ResNet-18 view tokens (hd 128, PointSea.py:188-229)
 ]
 
 

@@ -33,6 +33,12 @@ FPS_CASES = [
     ("tiny", 2, 37, 20),
     ("wave", 1, 64, 64),
     ("stream", 2, 20000, 300),
+    # work-pruned kernel (2048 < N <= 16384): each points-per-lane instance and its edges
+    ("p4096", 2, 4096, 1024),
+    ("p4097", 1, 4097, 900),
+    ("p55", 2, 8192, 2048),
+    ("p8193", 1, 8193, 1500),
+    ("p3001", 1, 3001, 777),
 ]
 
 
@@ -59,6 +65,38 @@ def test_fps_ties_and_zero_points_bitexact(dev):
     np.testing.assert_array_equal(got, O.furthest_point_sample(y, 2000))
     z = np.zeros((1, 1024, 3), np.float32)  # nothing valid -> index 0 everywhere
     assert (furthest_point_sample(T(z, dev), 16).cpu().numpy() == 0).all()
+
+
+@pytest.mark.parametrize("kind", ["tiled16384", "zeros8192", "clusters", "line", "all_zero", "gauss16384"])
+def test_fps_pruned_edge_cases_bitexact(dev, kind):
+    """The work-pruned FPS (lanes skipped when their box cannot beat their running
+    distances) on the inputs that stress it: more samples than distinct points
+    (all running distances 0 -> the tie order alone decides), skipped |p|^2 <= 1e-3
+    points, far-apart clusters, a degenerate (flat) box, nothing valid at all."""
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
+
+    rng = np.random.default_rng(len(kind))
+    if kind == "tiled16384":
+        x, M = _tiled(rng, 2, 1500, 16384), 2048
+    elif kind == "zeros8192":
+        x, M = (rng.random((2, 8192, 3)) - 0.5).astype(np.float32), 8000
+        x[:, -1000:] = 0.0
+        x[:, 100:140] = 1e-2   # |p|^2 = 3e-4 <= 1e-3: skipped too
+    elif kind == "clusters":
+        x = (rng.standard_normal((2, 6000, 3)) * 1e-3).astype(np.float32)
+        x[:, ::2] += 100.0
+        x[:, 1::3] -= 50.0
+        M = 1500
+    elif kind == "line":
+        x = np.zeros((1, 5000, 3), np.float32)
+        x[0, :, 0] = np.linspace(-1, 1, 5000, dtype=np.float32)
+        M = 600
+    elif kind == "all_zero":
+        x, M = np.zeros((1, 4096, 3), np.float32), 64
+    else:
+        x, M = (rng.standard_normal((4, 16384, 3)) * 0.45).astype(np.float32), 2048
+    got = furthest_point_sample(T(x, dev), M).cpu().numpy()
+    np.testing.assert_array_equal(got, O.furthest_point_sample(x, M))
 
 
 def test_fps_full_size_properties(dev):
