@@ -209,6 +209,12 @@ def kernel_work(name, a):
     if name == "sa_group_grad":  # g, gdt, idx, B, N, S, K, C, gp: zero gp, read g[..., 3:] + idx, scatter-add
         gdt, B, N, S, K, C = a[1], a[3], a[4], a[5], a[6], a[7]
         return float(4 * B * N * C + B * S * K * (4 + C * (es(gdt) + 4))), "GB/s", HBM_PEAK, "hbm"
+    if name == "edge_group":     # x, idx, B, N, K, C, out, odt: read the (B,N,C) cloud + the index, write 2C per row
+        B, N, K, C, odt = a[2], a[3], a[4], a[5], a[7]
+        return float(B * N * C * 4 + B * N * K * (4 + 2 * C * es(odt))), "GB/s", HBM_PEAK, "hbm"
+    if name == "edge_group_grad":  # g, gdt, idx, B, N, K, C, gx: read g once + idx, write gx, scatter-add C per row
+        gdt, B, N, K, C = a[1], a[3], a[4], a[5], a[6]
+        return float(B * N * K * (2 * C * es(gdt) + 4 + 4 * C) + B * N * C * 4), "GB/s", HBM_PEAK, "hbm"
     if name == "chamfer_3D.backward":  # xyz1, xyz2, B, n, m: per point read xyz, partner xyz, grad, idx; write own
         B, n, m = a[2], a[3], a[4]       # grad, scatter-add the partner's (12 + 12 + 4 + 4 + 12 + 12 B)
         return float(56 * B * (n + m)), "GB/s", HBM_PEAK, "hbm"
@@ -258,7 +264,7 @@ _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_d
             "transpose_add": "transpose_add", "pcsa_forward": "pcsa_fwd", "pcsa_backward": "pcsa_bwd",
             "gather_points": "gather_kernel", "gather_points_grad": "gather_grad_kernel",
             "group_points": "group_kernel", "group_points_grad": "group_grad_kernel",
-            "chamfer_3D.backward": "chamfer_grad", "points2depth": "depth_", "points2grid": "points2grid",
+            "chamfer_3D.backward": "chamfer_grad_seg", "points2depth": "depth_", "points2grid": "points2grid",
             "grid2image": "grid2image|image_normalize", "sa_group": "sa_group_kernel",
             "sa_group_grad": "sa_group_grad_kernel",
             # calls that launch several kernels: (every kernel of the call, the one launched once per call)
@@ -269,7 +275,10 @@ _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_d
             "conv3x3_fwd": r"conv3x3_fwd_kernel", "conv3x3_dgrad": r"conv3x3_fwd_kernel",
             "conv3x3_wgrad": (r"conv3x3_wgrad_kernel|conv3x3_wgrad_reduce", r"conv3x3_wgrad_kernel"),
             "add": r"add_kernel", "max_k": r"max_k_kernel", "max_k_grad": r"max_k_grad_kernel",
-            "gelu_bwd": (r"gelu_bwd_partial_kernel|colsum_final", r"gelu_bwd_partial_kernel")}
+            "gelu_bwd": (r"gelu_bwd_partial_kernel|colsum_final", r"gelu_bwd_partial_kernel"),
+            "edge_group": r"edge_group_kernel",
+            "edge_group_grad": (r"edge_group_grad_own_kernel|edge_group_grad_scatter_kernel",
+                                r"edge_group_grad_own_kernel")}
 
 
 def pmc_traffic(path, key, name):

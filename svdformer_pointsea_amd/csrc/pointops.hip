@@ -471,7 +471,10 @@ __global__ __launch_bounds__(256) void edge_group_grad_own_kernel(const void *__
 }
 
 // Backward, neighbour term: dx[b,idx[b,n,k],c] -= g[b,n,k,c] (the index_points /
-// group_points_grad scatter, token-major: a thread's V atomics hit one row).
+// group_points_grad scatter, token-major).  Launched with V = 1: consecutive lanes
+// add to consecutive channels of one destination row, so a wave-instruction's
+// atomics form one contiguous 256-B run (the full global-atomic rate); 8 channels
+// per lane made every instruction touch 8 rows 32 B apart (a fraction of it).
 template <int V, int DT>
 __global__ __launch_bounds__(256) void edge_group_grad_scatter_kernel(const void *__restrict__ g,
                                                                       const int *__restrict__ idx, int N, int K, int C,
@@ -554,8 +557,8 @@ void edge_group_grad_go(const void *g, const int *idx, int B, int N, int K, int 
   const long long pts = (long long)B * N, rows = pts * K;
   hipLaunchKernelGGL((edge_group_grad_own_kernel<V, DT>), dim3(grid_for_ll(pts * (C / V))), dim3(256), 0, s, g, K, C,
                      pts, dx);
-  hipLaunchKernelGGL((edge_group_grad_scatter_kernel<V, DT>), dim3(grid_for_ll(rows * (C / V))), dim3(256), 0, s, g,
-                     idx, N, K, C, rows, dx);
+  hipLaunchKernelGGL((edge_group_grad_scatter_kernel<1, DT>), dim3(grid_for_ll(rows * C)), dim3(256), 0, s, g, idx, N,
+                     K, C, rows, dx);
 }
 }  // namespace
 
