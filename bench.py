@@ -414,7 +414,11 @@ def cpu_baseline(wl, steps):
             times.append(time.perf_counter() - t0)
     med = sorted(times)[len(times) // 2]
     return {"value": 1.0 / med, "unit": "samples/s", "cores": nthreads, "kind": "port",
-            "cpu_model": _cpu_model(), "step_s": [round(t, 3) for t in times],
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "cores_note": ("threads = OMP_NUM_THREADS: the GPU pool grants a one-GPU job a 16-CPU share of the "
+                           "host (its OMP_NUM_THREADS); os.cpu_count() is the whole host's count"
+                           if "OMP_NUM_THREADS" in os.environ else "threads = os.cpu_count()"),
+            "step_s": [round(t, 3) for t in times],
             "sample": f"median of {steps} train steps of 1 {wl.name} sample (2048->{wl.n_out}) after 1 warm-up, "
                       f"fp32: torch CPU ({nthreads} threads) + oracle/pcops_oracle.c point ops (OpenMP, "
                       f"{nthreads} threads) + torch CPU attention"}
@@ -710,6 +714,12 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
         dist.barrier()
     torch.cuda.synchronize()
     progress(f"[{tag}] timing {steps} steps")
+    # PCOPS_TRACE_MARKS=1: a spin kernel on each side of the timed steps, so a rocprofv3 kernel
+    # trace can be cut to exactly the timed replays (tools/trace_window.py); outside the clock
+    marks = os.environ.get("PCOPS_TRACE_MARKS") == "1" and tag == "headline"
+    if marks:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     host = 0.0  # time the host spends issuing a step (launches are asynchronous)
     for _ in range(steps):
@@ -720,6 +730,9 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if marks:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     check_finite("the timed steps")
     if use_graph and kernel_timing:
         # ROCm torch refuses timing events inside a captured graph ("External

@@ -39,20 +39,22 @@ run_stage() {
              > "$OUT/bench_pointsea_sa.json" 2> "$OUT/bench_pointsea_sa.err" ;;
     bench_fp32) timeout -k 10 500 python bench.py --fp32 --batch 16 --no-cpu-baseline > "$OUT/bench_fp32.json" \
                   2> "$OUT/bench_fp32.err" ;;
-    trace) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-             python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32-leg > "$OUT/bench_traced.json" \
-             2> "$OUT/trace.err"
+    trace) PCOPS_TRACE_MARKS=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+             python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32-leg --no-extra-legs \
+             > "$OUT/bench_traced.json" 2> "$OUT/trace.err"
            rc=$?
+           [ $rc -eq 0 ] && python tools/trace_window.py "$(find "$OUT/trace" -name '*kernel_trace.csv' -print -quit)" 10 \
+             "$OUT/kernel_stats_replay.csv" > "$OUT/trace_window.txt" 2>&1
            find "$OUT/trace" -name '*kernel_trace.csv' -exec gzip -9 {} +   # keep the merge-back small
            [ $rc -eq 0 ] || tail -30 "$OUT/trace.err"
            return $rc ;;
     pmc_traffic)
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
         -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
-        --no-fp32-leg > /dev/null 2> "$OUT/pmc_fetch.err" &&
+        --no-fp32-leg --no-extra-legs > /dev/null 2> "$OUT/pmc_fetch.err" &&
       timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
         -d "$OUT/pmc_write" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
-        --no-fp32-leg > /dev/null 2> "$OUT/pmc_write.err" &&
+        --no-fp32-leg --no-extra-legs > /dev/null 2> "$OUT/pmc_write.err" &&
       python tools/pmc_traffic.py "$(find "$OUT/pmc_fetch" -name '*counter_collection.csv' -print -quit)" \
         "$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)" "$OUT/pmc_traffic.json" &&
       find "$OUT/pmc_fetch" "$OUT/pmc_write" -name '*.csv' -exec gzip -9 {} + ;;
@@ -64,7 +66,7 @@ run_stage() {
       python tools/pmc_attn.py "$(find "$OUT/pmc_attn" -name '*counter_collection.csv' -print -quit)" \
         > "$OUT/pmc_attn_summary.json" ;;
     dist1) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
-             --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg \
+             --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg --no-extra-legs \
              > "$OUT/bench_dist1.json" 2> "$OUT/bench_dist1.err" ;;
     pmc_attn2)
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
@@ -84,7 +86,7 @@ run_stage() {
       IFS=';' read -ra groups <<< "${BENCH_AB:?set BENCH_AB}"
       for g in "${groups[@]}"; do
         echo "== $g" >> "$OUT/bench_ab.txt"
-        env $g timeout -k 10 400 python bench.py --no-cpu-baseline --no-fp32-leg --no-kernel-timing --steps 20 \
+        env $g timeout -k 10 400 python bench.py --no-cpu-baseline --no-fp32-leg --no-extra-legs --no-kernel-timing --steps 20 \
           --warmup 3 >> "$OUT/bench_ab.txt" 2>> "$OUT/bench_ab.err" || return 1
       done ;;
     avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
