@@ -396,7 +396,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
     }
     lmax = m;
     lhi = m >= 0.f ? __float_as_int(m) : 0;
-    llo = m >= 0.f ? (int)l : 0;
+    llo = (int)((m >= 0.f ? l : 0u) ^ 0x80000000u);  // sign-flipped: unsigned order under signed max
   };
   lane_best();
   int whi = 0, wlo = 0;
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
     }
     if (__any(changed)) wave_best();
     if (lane == 0) {
-      skey2[par][w] = make_uint2((unsigned)whi, (unsigned)wlo);
+      skey2[par][w] = make_uint2((unsigned)whi, (unsigned)wlo ^ 0x80000000u);
       sxyz2[par][w] = make_float4(wcx, wcy, wcz, 0.f);
     }
     lds_barrier();
