@@ -232,7 +232,6 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
 // bitrev_L(k mod T) * R + k div T (smaller wins), folded into the key
 //   hi = running distance bits (>= 0),  lo = (16383 - P) << 18 | wave << 14 | k
 // and the round's winner is the max 64-bit key over the cloud.
-constexpr int kPruneThreads = 1024;
 constexpr int kCellBits = 4;                       // per axis: 16^3 = 4096 Morton cells
 constexpr int kCells = 1 << (3 * kCellBits);
 
@@ -240,15 +239,15 @@ __device__ __forceinline__ unsigned spread3(unsigned v) {  // 4 bits -> every th
   return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
 }
 
-template <int PPT>
-__global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *__restrict__ xyz, int N, int M, int T,
+template <int NT, int PPT>
+__global__ __launch_bounds__(NT) void fps_prune_kernel(const float *__restrict__ xyz, int N, int M, int T,
                                                                   int L, int R, int *__restrict__ idx) {
   const int b = blockIdx.x;
   const float *p = xyz + (size_t)b * N * 3;
   int *out = idx + (size_t)b * M;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   __shared__ int cnt[kCells];
-  __shared__ unsigned short perm[kPruneThreads * PPT];
+  __shared__ unsigned short perm[NT * PPT];
   __shared__ float sred[6][16];
   __shared__ int sscan[16];
   __shared__ uint2 skey2[2][16];
@@ -258,7 +257,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
-    const int k = t + i * kPruneThreads;
+    const int k = t + i * NT;
     if (k < N) {
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
@@ -280,7 +279,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
       sred[3 + a][w] = mx[a];
     }
   }
-  for (int c = t; c < kCells; c += kPruneThreads) cnt[c] = 0;
+  for (int c = t; c < kCells; c += NT) cnt[c] = 0;
   if (t < 32) {
     skey2[t >> 4][t & 15] = make_uint2(0u, 0u);
     sxyz2[t >> 4][t & 15] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -302,7 +301,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
   int cell[PPT], pos[PPT];
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
-    const int k = t + i * kPruneThreads;
+    const int k = t + i * NT;
     cell[i] = 0;
     pos[i] = 0;
     if (k < N) {
@@ -317,9 +316,9 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
     }
   }
   __syncthreads();
-  // (3) exclusive scan of the cell counts (kCells / kPruneThreads per thread)
+  // (3) exclusive scan of the cell counts (kCells / NT per thread)
   {
-    constexpr int CPT = kCells / kPruneThreads;
+    constexpr int CPT = kCells / NT;
     int v[CPT], sum = 0;
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
@@ -346,7 +345,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
-    const int k = t + i * kPruneThreads;
+    const int k = t + i * NT;
     if (k < N) perm[cnt[cell[i]] + pos[i]] = (unsigned short)k;
   }
   __syncthreads();
@@ -380,7 +379,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
   }
   // the lane's best (running distance, priority) and its coordinates
   float lmax = -1.f, cx = 0.f, cy = 0.f, cz = 0.f;
-  int lhi = 0, llo = 0;
+  int lhi = 0, llo = 0, bi = 0;
   auto lane_best = [&]() {
     float m = -1.f;
 #pragma unroll
@@ -390,6 +389,7 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
     for (int i = 0; i < PPT; ++i) {
       const bool take = tmp[i] == m && lo[i] > l;
       l = take ? lo[i] : l;
+      bi = take ? i : bi;
       cx = take ? px[i] : cx;
       cy = take ? py[i] : cy;
       cz = take ? pz[i] : cz;
@@ -421,17 +421,19 @@ __global__ __launch_bounds__(kPruneThreads) void fps_prune_kernel(const float *_
     const float gy = fmaxf(fmaxf(by0 - oy, oy - by1), 0.f);
     const float gz = fmaxf(fmaxf(bz0 - oz, oz - bz1), 0.f);
     const float lb = gx * gx + gy * gy + gz * gz;
-    bool changed = false;
+    // the lane's (max, best) pair can only move when its best point's distance
+    // drops (the others only decrease, staying below it or dropping out of a tie)
+    bool moved = false;
     if (has && !(lb * kShrink > lmax)) {
 #pragma unroll
       for (int i = 0; i < PPT; ++i) {
         const float nt = fminf(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz), tmp[i]);
-        changed |= nt != tmp[i];
+        moved |= (i == bi) & (nt != tmp[i]);
         tmp[i] = nt;
       }
-      if (changed) lane_best();
+      if (moved) lane_best();
     }
-    if (__any(changed)) wave_best();
+    if (__any(moved)) wave_best();
     if (lane == 0) {
       skey2[par][w] = make_uint2((unsigned)whi, (unsigned)wlo ^ 0x80000000u);
       sxyz2[par][w] = make_float4(wcx, wcy, wcz, 0.f);
@@ -655,14 +657,29 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
   const int nthreads = T < 64 ? 64 : T;
   const int ppt = (N + T - 1) / T;  // points per reference thread
   hipStream_t s = (hipStream_t)stream;
-  if (N > 2048 && N <= kPruneThreads * 16 && fps_prune()) {
+  if (N > 2048 && N <= 16384 && fps_prune()) {
     const int R = (N + T - 1) / T;  // points per reference thread (P(k) = rev(k mod T) * R + k / T)
-    if (N <= kPruneThreads * 4)
-      hipLaunchKernelGGL(fps_prune_kernel<4>, dim3(B), dim3(kPruneThreads), 0, s, xyz, N, M, T, L, R, idx);
-    else if (N <= kPruneThreads * 8)
-      hipLaunchKernelGGL(fps_prune_kernel<8>, dim3(B), dim3(kPruneThreads), 0, s, xyz, N, M, T, L, R, idx);
-    else
-      hipLaunchKernelGGL(fps_prune_kernel<16>, dim3(B), dim3(kPruneThreads), 0, s, xyz, N, M, T, L, R, idx);
+    // 8 waves x up to 32 points per lane: with most of the sweep pruned the round is its fixed
+    // reduce / barrier cost, paid per wave (PCOPS_FPS_PRUNE_NT=1024: 16 waves x 16 points, A/B)
+    static const int nt = [] {
+      const char *e = getenv("PCOPS_FPS_PRUNE_NT");
+      return e ? atoi(e) : 512;
+    }();
+    if (nt == 1024) {
+      if (N <= 4096)
+        hipLaunchKernelGGL((fps_prune_kernel<1024, 4>), dim3(B), dim3(1024), 0, s, xyz, N, M, T, L, R, idx);
+      else if (N <= 8192)
+        hipLaunchKernelGGL((fps_prune_kernel<1024, 8>), dim3(B), dim3(1024), 0, s, xyz, N, M, T, L, R, idx);
+      else
+        hipLaunchKernelGGL((fps_prune_kernel<1024, 16>), dim3(B), dim3(1024), 0, s, xyz, N, M, T, L, R, idx);
+    } else {
+      if (N <= 4096)
+        hipLaunchKernelGGL((fps_prune_kernel<512, 8>), dim3(B), dim3(512), 0, s, xyz, N, M, T, L, R, idx);
+      else if (N <= 8192)
+        hipLaunchKernelGGL((fps_prune_kernel<512, 16>), dim3(B), dim3(512), 0, s, xyz, N, M, T, L, R, idx);
+      else
+        hipLaunchKernelGGL((fps_prune_kernel<512, 32>), dim3(B), dim3(512), 0, s, xyz, N, M, T, L, R, idx);
+    }
     PC_CHECK_LAUNCH();
     return PCOPS_OK;
   }

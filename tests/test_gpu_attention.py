@@ -74,9 +74,11 @@ def test_core_backward_fp32(dev, B, H, Lq, Lk, E):
     (attention_core(qs, ks, vs, H) * g).sum().backward()
     qd, kd, vd = [t.double().clone().requires_grad_(True) for t in (q, k, v)]
     (_ref(qd, kd, vd, H) * g.double()).sum().backward()
+    # the north-star bar, absolute: measured max |err| over SHAPES is 2.3e-6 (dk/dv at
+    # 2048 x 512, hd 64) against max |grad| 0.3-3.6 (tools/attn_err.py, profiles/r3_attn_err.jsonl)
     for a, b in [(qs.grad, qd.grad), (ks.grad, kd.grad), (vs.grad, vd.grad)]:
         err = (a.double() - b).abs().max().item()
-        assert err < 1e-4 * max(1.0, b.abs().max().item()), err
+        assert err < 1e-5, err
 
 
 @pytest.mark.parametrize("B,H,Lq,Lk,E", SHAPES)
@@ -443,9 +445,11 @@ def test_core_fp32_growing_row_max(dev, hd):
     gq = torch.randn(Lq, B, E, generator=torch.Generator().manual_seed(8)).to(dev)
     (o * gq).sum().backward()
     (ref * gq.double()).sum().backward()
+    # the north-star bar, absolute: measured max |err| over SHAPES is 2.3e-6 (dk/dv at
+    # 2048 x 512, hd 64) against max |grad| 0.3-3.6 (tools/attn_err.py, profiles/r3_attn_err.jsonl)
     for a, b in [(qs.grad, qd.grad), (ks.grad, kd.grad), (vs.grad, vd.grad)]:
         err = (a.double() - b).abs().max().item()
-        assert err < 1e-4 * max(1.0, b.abs().max().item()), err
+        assert err < 1e-5, err
 
 
 def _forward_lse(q, k, v, H):
