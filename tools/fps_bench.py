@@ -10,7 +10,7 @@ from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample  # noqa
 
 dev = torch.device("cuda", 0)
 g = torch.Generator(device="cpu").manual_seed(0)
-tag = "prune=" + os.environ.get("PCOPS_FPS_PRUNE", "1")
+tag = "prune=" + os.environ.get("PCOPS_FPS_PRUNE", "1") + " nt=" + os.environ.get("PCOPS_FPS_PRUNE_NT", "512")
 for B, N, M, kind in [(32, 16384, 2048, "gauss"), (32, 16384, 2048, "surface"), (16, 8192, 2048, "surface"),
                       (32, 2304, 512, "surface"), (32, 4096, 1024, "gauss")]:
     x = torch.randn(B, N, 3, generator=g)

@@ -91,8 +91,12 @@ run_stage() {
       done ;;
     avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
     knn) timeout -k 10 120 python tools/knn_bench.py > "$OUT/knn_bench.txt" 2>&1 ;;
-    fps_ab) for v in 0 1; do PCOPS_FPS_PRUNE=$v timeout -k 10 120 python tools/fps_bench.py >> "$OUT/fps_bench.txt" 2>&1 \
-              || return 1; done ;;
+    fps_ab)   # FPS times per env group in $FPS_AB ("A=1;A=0"), default pruned vs full sweep
+      IFS=';' read -ra groups <<< "${FPS_AB:-PCOPS_FPS_PRUNE=0;PCOPS_FPS_PRUNE=1}"
+      for g in "${groups[@]}"; do
+        echo "== $g" >> "$OUT/fps_bench.txt"
+        env $g timeout -k 10 120 python tools/fps_bench.py >> "$OUT/fps_bench.txt" 2>&1 || return 1
+      done ;;
     attn_err) timeout -k 10 300 python tools/attn_err.py > "$OUT/attn_err.jsonl" 2>&1 ;;
     chamfer) timeout -k 10 120 python tools/microbench.py > "$OUT/chamfer_bench.txt" 2>&1 ;;
     *) echo "unknown stage $1"; return 2 ;;
