@@ -221,13 +221,17 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
 // skipped.  The winner of a round depends only on the multiset of (running
 // distance, tie priority) pairs, so the points can sit anywhere: they are
 // bucketed by a 12-bit Morton cell of the cloud's box once (LDS counting sort;
-// the order inside a cell is arbitrary and irrelevant) and every lane holds
-// PPT spatially adjacent points plus their bounding box.  A round skips a lane
-// when the box's squared distance to the new centre, shrunk by a rounding
-// margin, exceeds the lane's largest running distance: then no point of the
-// lane can lower its running min (fl(d) >= exact d (1 - 5u) >= lb (1 - 11u)
-// for the reference's fp32 expression), so the skipped update would have
-// changed nothing.  Late rounds touch only the lanes around the new centre.
+// the order inside a cell is arbitrary and irrelevant) and cut into CHUNKS of
+// 64 consecutive sorted points -- one wave-instruction of the sweep each; a
+// wave owns PPT chunks (lane l holds point l of each).  A round sweeps a chunk
+// only when the squared distance from the new centre to the chunk's box,
+// shrunk by a rounding margin, does not exceed the chunk's largest running
+// distance: otherwise no point of the chunk can lower its running min (fl(d)
+// >= exact d (1 - 5u) >= lb (1 - 11u) for the reference's fp32 expression), so
+// the skipped sweep would have changed nothing.  All PPT box tests of a wave
+// are one VALU pass (lane i tests chunk i); late rounds sweep only the few
+// chunks around the new centre.  (Skipping per LANE does not pay: a wave runs
+// the sweep if any of its lanes needs it.)
 // Ties: point k's priority is the reference LDS tree's order, P(k) =
 // bitrev_L(k mod T) * R + k div T (smaller wins), folded into the key
 //   hi = running distance bits (>= 0),  lo = (16383 - P) << 18 | wave << 14 | k
@@ -350,14 +354,13 @@ __global__ __launch_bounds__(NT) void fps_prune_kernel(const float *__restrict__
   }
   __syncthreads();
 
-  // (4) this lane's PPT points (sorted slots t*PPT ...), their keys and box
+  // (4) chunk i of wave w = the sorted slots [64 (w PPT + i), + 64): lane l holds its point l.
+  //     A chunk is 64 spatially adjacent points, ONE wave-instruction of the sweep.
   float px[PPT], py[PPT], pz[PPT], tmp[PPT];
   unsigned lo[PPT];
-  float bx0 = INFINITY, by0 = INFINITY, bz0 = INFINITY, bx1 = -INFINITY, by1 = -INFINITY, bz1 = -INFINITY;
-  bool has = false;
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
-    const int s = t * PPT + i;
+    const int s = 64 * (w * PPT + i) + lane;
     px[i] = py[i] = pz[i] = 0.f;
     tmp[i] = -1.f;  // never competes
     lo[i] = 0u;
@@ -371,43 +374,47 @@ __global__ __launch_bounds__(NT) void fps_prune_kernel(const float *__restrict__
         tmp[i] = 1e10f;
         const unsigned P = bitrev_bits((unsigned)k & (unsigned)(T - 1), L) * (unsigned)R + ((unsigned)k >> L);
         lo[i] = ((16383u - P) << 18) | ((unsigned)w << 14) | (unsigned)k;
-        bx0 = fminf(bx0, px[i]), by0 = fminf(by0, py[i]), bz0 = fminf(bz0, pz[i]);
-        bx1 = fmaxf(bx1, px[i]), by1 = fmaxf(by1, py[i]), bz1 = fmaxf(bz1, pz[i]);
-        has = true;
       }
     }
   }
-  // the lane's best (running distance, priority) and its coordinates
-  float lmax = -1.f, cx = 0.f, cy = 0.f, cz = 0.f;
-  int lhi = 0, llo = 0, bi = 0;
-  auto lane_best = [&]() {
-    float m = -1.f;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) m = fmaxf(m, tmp[i]);
-    unsigned l = 0u;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const bool take = tmp[i] == m && lo[i] > l;
-      l = take ? lo[i] : l;
-      bi = take ? i : bi;
-      cx = take ? px[i] : cx;
-      cy = take ? py[i] : cy;
-      cz = take ? pz[i] : cz;
+  // chunk summaries, chunk i's held by lane i: box, max running distance, best key + coords
+  float cb0 = INFINITY, cb1 = INFINITY, cb2 = INFINITY, cb3 = -INFINITY, cb4 = -INFINITY, cb5 = -INFINITY;
+  float cmax = -1.f, ccx = 0.f, ccy = 0.f, ccz = 0.f;
+  int chi = 0, clo = INT_MIN;   // clo: the key's low word, sign-flipped (unsigned order under signed max)
+  auto chunk_summary = [&](int i) {
+    const int bits = __float_as_int(tmp[i]);  // -1.0 (never) is negative
+    const int hi = wave_max_i32(bits);
+    const int ls = wave_max_i32(bits == hi ? (int)(lo[i] ^ 0x80000000u) : INT_MIN);
+    const int wl = (int)__builtin_ctzll(__ballot(bits == hi && (int)(lo[i] ^ 0x80000000u) == ls));
+    const float bx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[i]), wl));
+    const float by = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[i]), wl));
+    const float bz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[i]), wl));
+    if (lane == i) {
+      cmax = hi >= 0 ? __int_as_float(hi) : -1.f;
+      chi = hi >= 0 ? hi : 0;
+      clo = hi >= 0 ? ls : INT_MIN;
+      ccx = bx, ccy = by, ccz = bz;
     }
-    lmax = m;
-    lhi = m >= 0.f ? __float_as_int(m) : 0;
-    llo = (int)((m >= 0.f ? l : 0u) ^ 0x80000000u);  // sign-flipped: unsigned order under signed max
   };
-  lane_best();
-  int whi = 0, wlo = 0;
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const bool v = tmp[i] >= 0.f;
+    const float x0m = wave_min_f32(v ? px[i] : INFINITY), x1m = wave_max_f32(v ? px[i] : -INFINITY);
+    const float y0m = wave_min_f32(v ? py[i] : INFINITY), y1m = wave_max_f32(v ? py[i] : -INFINITY);
+    const float z0m = wave_min_f32(v ? pz[i] : INFINITY), z1m = wave_max_f32(v ? pz[i] : -INFINITY);
+    if (lane == i) cb0 = x0m, cb1 = y0m, cb2 = z0m, cb3 = x1m, cb4 = y1m, cb5 = z1m;
+    chunk_summary(i);
+  }
+  int whi = 0, wlo = INT_MIN;
   float wcx = 0.f, wcy = 0.f, wcz = 0.f;
   auto wave_best = [&]() {
-    whi = wave_max_i32(lhi);
-    wlo = wave_max_i32(lhi == whi ? llo : INT_MIN);
-    const int wl = (int)__builtin_ctzll(__ballot(lhi == whi && llo == wlo));
-    wcx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), wl));
-    wcy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), wl));
-    wcz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cz), wl));
+    const bool own = lane < PPT;
+    whi = wave_max_i32(own ? chi : INT_MIN);
+    wlo = wave_max_i32(own && chi == whi ? clo : INT_MIN);
+    const int wl = (int)__builtin_ctzll(__ballot(own && chi == whi && clo == wlo));
+    wcx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ccx), wl));
+    wcy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ccy), wl));
+    wcz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ccz), wl));
   };
   wave_best();
 
@@ -417,29 +424,29 @@ __global__ __launch_bounds__(NT) void fps_prune_kernel(const float *__restrict__
   constexpr float kShrink = 1.f - 1.f / 262144.f;  // 2^-18 >> the 11u rounding margin
   for (int j = 1; j < M; ++j) {
     const int par = j & 1;
-    const float gx = fmaxf(fmaxf(bx0 - ox, ox - bx1), 0.f);
-    const float gy = fmaxf(fmaxf(by0 - oy, oy - by1), 0.f);
-    const float gz = fmaxf(fmaxf(bz0 - oz, oz - bz1), 0.f);
+    // every chunk's box test at once (lane i tests chunk i); a chunk is swept only if the
+    // new centre can come within its largest running distance
+    const float gx = fmaxf(fmaxf(cb0 - ox, ox - cb3), 0.f);
+    const float gy = fmaxf(fmaxf(cb1 - oy, oy - cb4), 0.f);
+    const float gz = fmaxf(fmaxf(cb2 - oz, oz - cb5), 0.f);
     const float lb = gx * gx + gy * gy + gz * gz;
-    // the lane's (max, best) pair can only move when its best point's distance
-    // drops (the others only decrease, staying below it or dropping out of a tie)
-    bool moved = false;
-    if (has && !(lb * kShrink > lmax)) {
+    const uint64_t mask = __ballot(lane < PPT && cmax >= 0.f && !(lb * kShrink > cmax));
+    if (mask) {
 #pragma unroll
       for (int i = 0; i < PPT; ++i) {
-        const float nt = fminf(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz), tmp[i]);
-        moved |= (i == bi) & (nt != tmp[i]);
-        tmp[i] = nt;
+        if ((mask >> i) & 1ull) {  // wave-uniform
+          tmp[i] = fminf(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz), tmp[i]);
+          chunk_summary(i);
+        }
       }
-      if (moved) lane_best();
+      wave_best();
     }
-    if (__any(moved)) wave_best();
     if (lane == 0) {
       skey2[par][w] = make_uint2((unsigned)whi, (unsigned)wlo ^ 0x80000000u);
       sxyz2[par][w] = make_float4(wcx, wcy, wcz, 0.f);
     }
     lds_barrier();
-    // 64-bit max over the 16 wave slots in one DPP row (every wave, no second barrier)
+    // 64-bit max over the wave slots in one DPP row (every wave, no second barrier)
     const uint2 kv = skey2[par][lane & 15];
     const float4 cv = sxyz2[par][lane & 15];
     unsigned long long key = ((unsigned long long)kv.x << 32) | kv.y;
