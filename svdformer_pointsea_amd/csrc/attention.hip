@@ -699,175 +699,6 @@ int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse
   }
 }
 
-// ----------------------------------------------------------------- forward, bf16 (v3)
-// attn_fwd2 with TWO 32-query blocks per wave: every K fragment (ds_read_b128) and
-// every transposed V fragment (ds_read_b64_tr_b16) read from LDS feeds two MFMAs
-// instead of one -- half the LDS traffic per MFMA -- and the two blocks' softmax
-// VALU work interleaves with the other block's MFMAs.  Per query block the
-// arithmetic is fwd2's, in the same order (the deferred-rescale decision is taken
-// per block, as fwd2 takes it per wave), so O and the LSE are bitwise fwd2's.
-
-// acc[hf][b] += Rows(32 x D, tile half hf) . Ent_b for query blocks b = 0, 1
-template <int D>
-__device__ __forceinline__ void k_product22(f32x16 (&acc)[2][2], const __bf16 *lds0, const __bf16 *lds1,
-                                            const bf16x8 (&fa)[D / 16], const bf16x8 (&fb)[D / 16]) {
-  const int l = lane_(), h = l >> 5, row = l & 31;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8 *>(lds0 + img_off<D>(row, 2 * s + h));
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8 *>(lds1 + img_off<D>(row, 2 * s + h));
-    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, fa[s], acc[0][0], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fa[s], acc[1][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, fb[s], acc[0][1], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, fb[s], acc[1][1], 0, 0, 0);
-  }
-}
-
-// YA[db] += Rows^T . XA and YB[db] += Rows^T . XB, each transposed fragment read once
-template <int D>
-__device__ __forceinline__ void v_product_2(f32x16 (&YA)[D / 32], f32x16 (&YB)[D / 32], const __bf16 *lds,
-                                            const f32x16 &XA, const f32x16 &XB) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
-  typedef __attribute__((address_space(3))) short4v lds_s4;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    bf16x8 ba, bb;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      ba[e] = (__bf16)XA[8 * s + e];
-      bb[e] = (__bf16)XB[8 * s + e];
-    }
-    const int row0 = 16 * s + 4 * h + q;
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      const int ch = 4 * db + 2 * g + (p >> 1), e = 4 * (p & 1);
-      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0, ch) + e));
-      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0 + 8, ch) + e));
-      const bf16x8 a = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1,
-                                               2, 3, 4, 5, 6, 7);
-      YA[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ba, YA[db], 0, 0, 0);
-      YB[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, YB[db], 0, 0, 0);
-    }
-  }
-#endif
-}
-
-template <int D, int NW, int OCC>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void attn_fwd3_kernel(
-    const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K, const __bf16 *__restrict__ V, __bf16 *__restrict__ O,
-    float *__restrict__ lse, int Lq, int Lk, float scale, Strides st) {
-  using C = Fwd2Cfg<D, NW>;
-  extern __shared__ __attribute__((aligned(16))) unsigned char fwd3_smem[];
-  __bf16 *sk = reinterpret_cast<__bf16 *>(fwd3_smem);
-  __bf16 *sv = sk + 2 * C::kKBuf;
-  int rb, bh;
-  xcd_block(rb, bh);
-  const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
-  const int q0 = rb * (NW * 64) + w * 64;   // block b: queries q0 + 32 b + (l & 31)
-  bf16x8 qf[2][D / 16];
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int qi = q0 + 32 * b + (l & 31);
-    const __bf16 *row = Q + st.q_off(bh) + (long long)(qi < Lq ? qi : 0) * st.q_srow + 8 * h;
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-      qf[b][s] = qi < Lq ? *reinterpret_cast<const bf16x8 *>(row + 16 * s) : bf16x8{};
-  }
-  const __bf16 *Kb = K + st.k_off(bh);
-  const __bf16 *Vb = V + st.v_off(bh);
-  const float sl2 = scale * kLog2e;
-  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
-  f32x16 Y[2][D / 32];
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) Y[b][db] = f32x16{};
-  typename C::Regs kr, vr;
-  fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
-  fwd2_store<D, NW>(sk, sv, kr, vr);
-  lds_barrier();
-  const int ntiles = (Lk + kKT - 1) / kKT;
-  auto tile = [&](int t, auto edge_c) {
-    constexpr bool EDGE = decltype(edge_c)::value;
-    const int cur = t & 1;
-    const int k0 = t * kKT;
-    if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
-    const __bf16 *ck = sk + cur * C::kKBuf;
-    const __bf16 *cv = sv + cur * C::kVBuf;
-    f32x16 X[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) X[a][0] = X[a][1] = f32x16{};
-    k_product22<D>(X, ck, ck + 32 * C::kKS, qf[0], qf[1]);
-    if constexpr (EDGE) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (k0 + acc_row(r, h) >= Lk) X[0][0][r] = X[0][1][r] = -INFINITY;
-        if (k0 + 32 + acc_row(r, h) >= Lk) X[1][0][r] = X[1][1][r] = -INFINITY;
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) tmax = max3_raw(tmax, X[0][b][r], X[1][b][r]);
-      tmax = swap_halves_max(tmax);
-      const float pm = tmax * sl2;
-      const bool keep = __all(pm - m[b] <= kDeferLog2);
-      const float mn = keep ? m[b] : fmaxf(m[b], pm);
-      const float alpha = keep ? 1.f : exp2_ftz(m[b] - mn);
-      float rs = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        X[0][b][r] = exp2_ftz(__builtin_fmaf(X[0][b][r], sl2, -mn));
-        X[1][b][r] = exp2_ftz(__builtin_fmaf(X[1][b][r], sl2, -mn));
-        rs += X[0][b][r] + X[1][b][r];
-      }
-      rs = swap_halves_sum(rs);
-      lsum[b] = lsum[b] * alpha + rs;
-      m[b] = mn;
-      if (!keep) {
-#pragma unroll
-        for (int db = 0; db < D / 32; ++db) Y[b][db] *= alpha;
-      }
-    }
-    v_product_2<D>(Y[0], Y[1], cv, X[0][0], X[0][1]);
-    v_product_2<D>(Y[0], Y[1], cv + 32 * C::kVS, X[1][0], X[1][1]);
-    if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
-    lds_barrier();
-  };
-  const int nfull = Lk / kKT;
-  for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
-  if (nfull < ntiles) tile(nfull, std::true_type{});
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    store_Y<__bf16, D>(Y[b], O + st.o_off(bh), st.o_srow, q0 + 32 * b, Lq, 1.f / lsum[b]);
-    const int qi = q0 + 32 * b + (l & 31);
-    if (h == 0 && qi < Lq && lse) lse[(long long)bh * Lq + qi] = (m[b] + log2f(lsum[b])) * kLn2;
-  }
-}
-
-template <int D, int NW, int OCC>
-int launch_fwd3(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, float scale,
-                const Strides &st, hipStream_t s) {
-  using C = Fwd2Cfg<D, NW>;
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_fwd3_kernel<D, NW, OCC>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
-  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
-  const dim3 grid((Lq + NW * 64 - 1) / (NW * 64), BH);
-  hipLaunchKernelGGL((attn_fwd3_kernel<D, NW, OCC>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
-                     (const __bf16 *)k, (const __bf16 *)v, (__bf16 *)o, lse, Lq, Lk, scale, st);
-  PC_CHECK_LAUNCH();
-  return PCOPS_OK;
-}
-
-// PCOPS_FWD3 (read per call, so tests can compare the two forms in one process):
-// 0 = fwd2; 1 = fwd3 with 4-wave blocks; 2 = fwd3 with 8-wave blocks
-int fwd3_mode() {
-  const char *e = getenv("PCOPS_FWD3");
-  return e ? atoi(e) : 0;
-}
-
 // ----------------------------------------------------------------- backward, bf16 (v2)
 // dQ pass: queries on the lane, K/V 64-row tiles double-buffered (as forward).
 // FD (fused delta): the lane's delta = rowsum(dO * O) is formed from the dO
@@ -1268,12 +1099,6 @@ int dkv2_dispatch(const void *q, const void *k, const void *v, const void *dout,
 int fwd2_dispatch(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, int D,
                   float scale, const Strides &st, hipStream_t s) {
   const bool wide = Lq > 128;
-  if (wide) {
-    const int f3 = fwd3_mode();
-    if (f3 == 1 && D == 64) return launch_fwd3<64, 4, 2>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
-    if (f3 == 2 && D == 64) return launch_fwd3<64, 8, 2>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
-    // D >= 96: two blocks' accumulators do not fit 256 registers (D = 128 spilled at 512)
-  }
   switch (D) {
     case 32:
       return wide ? launch_fwd2<32, 8>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s)

@@ -216,276 +216,6 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
   FPS_STAMP_FLUSH
 }
 
-// ---- work-pruned FPS (2048 < N <= 16384) ---------------------------------
-// Same result as fps_reg_kernel, bit for bit, with most of each round's sweep
-// skipped.  The winner of a round depends only on the multiset of (running
-// distance, tie priority) pairs, so the points can sit anywhere: they are
-// bucketed by a 12-bit Morton cell of the cloud's box once (LDS counting sort;
-// the order inside a cell is arbitrary and irrelevant) and cut into CHUNKS of
-// 64 consecutive sorted points -- one wave-instruction of the sweep each; a
-// wave owns PPT chunks (lane l holds point l of each).  A round sweeps a chunk
-// only when the squared distance from the new centre to the chunk's box,
-// shrunk by a rounding margin, does not exceed the chunk's largest running
-// distance: otherwise no point of the chunk can lower its running min (fl(d)
-// >= exact d (1 - 5u) >= lb (1 - 11u) for the reference's fp32 expression), so
-// the skipped sweep would have changed nothing.  All PPT box tests of a wave
-// are one VALU pass (lane i tests chunk i); late rounds sweep only the few
-// chunks around the new centre.  (Skipping per LANE does not pay: a wave runs
-// the sweep if any of its lanes needs it.)
-// Ties: point k's priority is the reference LDS tree's order, P(k) =
-// bitrev_L(k mod T) * R + k div T (smaller wins), folded into the key
-//   hi = running distance bits (>= 0),  lo = (16383 - P) << 18 | wave << 14 | k
-// and the round's winner is the max 64-bit key over the cloud.
-constexpr int kCellBits = 4;                       // per axis: 16^3 = 4096 Morton cells
-constexpr int kCells = 1 << (3 * kCellBits);
-
-__device__ __forceinline__ unsigned spread3(unsigned v) {  // 4 bits -> every third bit
-  return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
-}
-
-template <int NT, int PPT>
-__global__ __launch_bounds__(NT) void fps_prune_kernel(const float *__restrict__ xyz, int N, int M, int T,
-                                                                  int L, int R, int *__restrict__ idx) {
-  const int b = blockIdx.x;
-  const float *p = xyz + (size_t)b * N * 3;
-  int *out = idx + (size_t)b * M;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  __shared__ int cnt[kCells];
-  __shared__ unsigned short perm[NT * PPT];
-  __shared__ float sred[6][16];
-  __shared__ int sscan[16];
-  __shared__ uint2 skey2[2][16];
-  __shared__ float4 sxyz2[2][16];
-
-  // (1) the cloud's box (fminf / fmaxf drop NaN coordinates)
-  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + i * NT;
-    if (k < N) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const float v = p[3 * k + a];
-        mn[a] = fminf(mn[a], v);
-        mx[a] = fmaxf(mx[a], v);
-      }
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    mn[a] = wave_min_f32(mn[a]);
-    mx[a] = wave_max_f32(mx[a]);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      sred[a][w] = mn[a];
-      sred[3 + a][w] = mx[a];
-    }
-  }
-  for (int c = t; c < kCells; c += NT) cnt[c] = 0;
-  if (t < 32) {
-    skey2[t >> 4][t & 15] = make_uint2(0u, 0u);
-    sxyz2[t >> 4][t & 15] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  __syncthreads();
-  float org[3], scl[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    float lo = sred[a][0], hi = sred[3 + a][0];
-    for (int ww = 1; ww < 16; ++ww) {
-      lo = fminf(lo, sred[a][ww]);
-      hi = fmaxf(hi, sred[3 + a][ww]);
-    }
-    const float ext = hi - lo;
-    org[a] = lo;
-    scl[a] = ext > 0.f && ext < INFINITY ? (float)(1 << kCellBits) / ext : 0.f;
-  }
-  // (2) Morton cell of every point and its slot inside the cell
-  int cell[PPT], pos[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + i * NT;
-    cell[i] = 0;
-    pos[i] = 0;
-    if (k < N) {
-      unsigned q[3];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const float f = fminf(fmaxf((p[3 * k + a] - org[a]) * scl[a], 0.f), (float)((1 << kCellBits) - 1));
-        q[a] = (unsigned)f;  // NaN -> fmaxf -> 0
-      }
-      cell[i] = (int)(spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2));
-      pos[i] = atomicAdd(&cnt[cell[i]], 1);
-    }
-  }
-  __syncthreads();
-  // (3) exclusive scan of the cell counts (kCells / NT per thread)
-  {
-    constexpr int CPT = kCells / NT;
-    int v[CPT], sum = 0;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      v[c] = cnt[t * CPT + c];
-      sum += v[c];
-    }
-    int incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += u;
-    }
-    if (lane == 63) sscan[w] = incl;
-    __syncthreads();
-    int base = 0;
-    for (int ww = 0; ww < w; ++ww) base += sscan[ww];
-    int run = base + incl - sum;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      cnt[t * CPT + c] = run;
-      run += v[c];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + i * NT;
-    if (k < N) perm[cnt[cell[i]] + pos[i]] = (unsigned short)k;
-  }
-  __syncthreads();
-
-  // (4) chunk i of wave w = the sorted slots [64 (w PPT + i), + 64): lane l holds its point l.
-  //     A chunk is 64 spatially adjacent points, ONE wave-instruction of the sweep.
-  float px[PPT], py[PPT], pz[PPT], tmp[PPT];
-  unsigned lo[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int s = 64 * (w * PPT + i) + lane;
-    px[i] = py[i] = pz[i] = 0.f;
-    tmp[i] = -1.f;  // never competes
-    lo[i] = 0u;
-    if (s < N) {
-      const int k = perm[s];
-      px[i] = p[3 * k];
-      py[i] = p[3 * k + 1];
-      pz[i] = p[3 * k + 2];
-      const float mag = sqd3(px[i], py[i], pz[i]);
-      if (!((double)mag <= 1e-3)) {  // sampling_gpu.cu:100-101
-        tmp[i] = 1e10f;
-        const unsigned P = bitrev_bits((unsigned)k & (unsigned)(T - 1), L) * (unsigned)R + ((unsigned)k >> L);
-        lo[i] = ((16383u - P) << 18) | ((unsigned)w << 14) | (unsigned)k;
-      }
-    }
-  }
-  // chunk summaries, chunk i's held by lane i: box, max running distance, best key + coords
-  float cb0 = INFINITY, cb1 = INFINITY, cb2 = INFINITY, cb3 = -INFINITY, cb4 = -INFINITY, cb5 = -INFINITY;
-  float cmax = -1.f, ccx = 0.f, ccy = 0.f, ccz = 0.f;
-  int chi = 0, clo = INT_MIN;   // clo: the key's low word, sign-flipped (unsigned order under signed max)
-  auto chunk_summary = [&](int i) {
-    const int bits = __float_as_int(tmp[i]);  // -1.0 (never) is negative
-    const int hi = wave_max_i32(bits);
-    const int ls = wave_max_i32(bits == hi ? (int)(lo[i] ^ 0x80000000u) : INT_MIN);
-    const int wl = (int)__builtin_ctzll(__ballot(bits == hi && (int)(lo[i] ^ 0x80000000u) == ls));
-    const float bx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[i]), wl));
-    const float by = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[i]), wl));
-    const float bz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[i]), wl));
-    if (lane == i) {
-      cmax = hi >= 0 ? __int_as_float(hi) : -1.f;
-      chi = hi >= 0 ? hi : 0;
-      clo = hi >= 0 ? ls : INT_MIN;
-      ccx = bx, ccy = by, ccz = bz;
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const bool v = tmp[i] >= 0.f;
-    const float x0m = wave_min_f32(v ? px[i] : INFINITY), x1m = wave_max_f32(v ? px[i] : -INFINITY);
-    const float y0m = wave_min_f32(v ? py[i] : INFINITY), y1m = wave_max_f32(v ? py[i] : -INFINITY);
-    const float z0m = wave_min_f32(v ? pz[i] : INFINITY), z1m = wave_max_f32(v ? pz[i] : -INFINITY);
-    if (lane == i) cb0 = x0m, cb1 = y0m, cb2 = z0m, cb3 = x1m, cb4 = y1m, cb5 = z1m;
-    chunk_summary(i);
-  }
-  int whi = 0, wlo = INT_MIN;
-  float wcx = 0.f, wcy = 0.f, wcz = 0.f;
-  auto wave_best = [&]() {
-    const bool own = lane < PPT;
-    whi = wave_max_i32(own ? chi : INT_MIN);
-    wlo = wave_max_i32(own && chi == whi ? clo : INT_MIN);
-    const int wl = (int)__builtin_ctzll(__ballot(own && chi == whi && clo == wlo));
-    wcx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ccx), wl));
-    wcy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ccy), wl));
-    wcz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ccz), wl));
-  };
-  wave_best();
-
-  const float x0 = p[0], y0 = p[1], z0 = p[2];
-  float ox = x0, oy = y0, oz = z0;
-  if (t == 0 && M > 0) out[0] = 0;
-  constexpr float kShrink = 1.f - 1.f / 262144.f;  // 2^-18 >> the 11u rounding margin
-  for (int j = 1; j < M; ++j) {
-    const int par = j & 1;
-    // every chunk's box test at once (lane i tests chunk i); a chunk is swept only if the
-    // new centre can come within its largest running distance
-    const float gx = fmaxf(fmaxf(cb0 - ox, ox - cb3), 0.f);
-    const float gy = fmaxf(fmaxf(cb1 - oy, oy - cb4), 0.f);
-    const float gz = fmaxf(fmaxf(cb2 - oz, oz - cb5), 0.f);
-    const float lb = gx * gx + gy * gy + gz * gz;
-    const uint64_t mask = __ballot(lane < PPT && cmax >= 0.f && !(lb * kShrink > cmax));
-    if (mask) {
-#pragma unroll
-      for (int i = 0; i < PPT; ++i) {
-        if ((mask >> i) & 1ull) {  // wave-uniform
-          tmp[i] = fminf(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz), tmp[i]);
-          chunk_summary(i);
-        }
-      }
-      wave_best();
-    }
-    if (lane == 0) {
-      skey2[par][w] = make_uint2((unsigned)whi, (unsigned)wlo ^ 0x80000000u);
-      sxyz2[par][w] = make_float4(wcx, wcy, wcz, 0.f);
-    }
-    lds_barrier();
-    // 64-bit max over the wave slots in one DPP row (every wave, no second barrier)
-    const uint2 kv = skey2[par][lane & 15];
-    const float4 cv = sxyz2[par][lane & 15];
-    unsigned long long key = ((unsigned long long)kv.x << 32) | kv.y;
-#define FPS_DPP_MAX(CTRL)                                                                                   \
-  {                                                                                                        \
-    const unsigned hi2 = __builtin_amdgcn_update_dpp(0, (int)(key >> 32), CTRL, 0xF, 0xF, false);          \
-    const unsigned lo2 = __builtin_amdgcn_update_dpp(0, (int)(unsigned)key, CTRL, 0xF, 0xF, false);        \
-    const unsigned long long o = ((unsigned long long)hi2 << 32) | lo2;                                    \
-    key = o > key ? o : key;                                                                               \
-  }
-    FPS_DPP_MAX(0xB1)
-    FPS_DPP_MAX(0x4E)
-    FPS_DPP_MAX(0x141)
-    FPS_DPP_MAX(0x140)
-#undef FPS_DPP_MAX
-    const unsigned ghi = __builtin_amdgcn_readfirstlane((unsigned)(key >> 32));
-    const unsigned glo = __builtin_amdgcn_readfirstlane((unsigned)key);
-    int k = 0;
-    if (ghi != 0u || glo != 0u) {
-      const int gw = (int)((glo >> 14) & 15u);
-      k = (int)(glo & 0x3FFFu);
-      ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.x), gw));
-      oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.y), gw));
-      oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv.z), gw));
-    } else {  // no valid point at all: the reference's dists_i[0] == 0
-      ox = x0, oy = y0, oz = z0;
-    }
-    if (t == 0) out[j] = k;
-  }
-}
-
-bool fps_prune() {  // PCOPS_FPS_PRUNE=0: the full-sweep kernels for every N (A/B runs)
-  static const bool v = [] {
-    const char *e = getenv("PCOPS_FPS_PRUNE");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 struct __align__(16) FpsSlot {
   float d, x, y, z;
   int k;
@@ -664,32 +394,6 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
   const int nthreads = T < 64 ? 64 : T;
   const int ppt = (N + T - 1) / T;  // points per reference thread
   hipStream_t s = (hipStream_t)stream;
-  if (N > 2048 && N <= 16384 && fps_prune()) {
-    const int R = (N + T - 1) / T;  // points per reference thread (P(k) = rev(k mod T) * R + k / T)
-    // 8 waves x up to 32 points per lane: with most of the sweep pruned the round is its fixed
-    // reduce / barrier cost, paid per wave (PCOPS_FPS_PRUNE_NT=1024: 16 waves x 16 points, A/B)
-    static const int nt = [] {
-      const char *e = getenv("PCOPS_FPS_PRUNE_NT");
-      return e ? atoi(e) : 512;
-    }();
-    if (nt == 1024) {
-      if (N <= 4096)
-        hipLaunchKernelGGL((fps_prune_kernel<1024, 4>), dim3(B), dim3(1024), 0, s, xyz, N, M, T, L, R, idx);
-      else if (N <= 8192)
-        hipLaunchKernelGGL((fps_prune_kernel<1024, 8>), dim3(B), dim3(1024), 0, s, xyz, N, M, T, L, R, idx);
-      else
-        hipLaunchKernelGGL((fps_prune_kernel<1024, 16>), dim3(B), dim3(1024), 0, s, xyz, N, M, T, L, R, idx);
-    } else {
-      if (N <= 4096)
-        hipLaunchKernelGGL((fps_prune_kernel<512, 8>), dim3(B), dim3(512), 0, s, xyz, N, M, T, L, R, idx);
-      else if (N <= 8192)
-        hipLaunchKernelGGL((fps_prune_kernel<512, 16>), dim3(B), dim3(512), 0, s, xyz, N, M, T, L, R, idx);
-      else
-        hipLaunchKernelGGL((fps_prune_kernel<512, 32>), dim3(B), dim3(512), 0, s, xyz, N, M, T, L, R, idx);
-    }
-    PC_CHECK_LAUNCH();
-    return PCOPS_OK;
-  }
   if (ppt <= kFpsMaxPPT) {
     // clouds with > 16 points per reference thread use 2 hardware threads per
     // reference thread (1024 threads, 4 waves / SIMD).  Up to 16 the 8-wave

@@ -706,19 +706,3 @@ def test_gelu_backward_kernel(dev, dt, rows, C):
     assert A._take_sum(du) is None   # handed over exactly once
     torch.testing.assert_close(dsum, du.float().sum(0), rtol=1e-4, atol=1e-3)
 
-
-@pytest.mark.parametrize("mode", ["1", "2"])
-@pytest.mark.parametrize("B,H,Lq,Lk,E", [(2, 8, 2048, 2048, 512), (1, 8, 2048, 512, 512), (1, 8, 333, 250, 512),
-                                         (2, 8, 200, 77, 512)])
-def test_fwd3_bitwise_equals_fwd2(dev, monkeypatch, mode, B, H, Lq, Lk, E):
-    """attn_fwd3 (two query blocks per wave sharing each LDS fragment) computes each
-    query's output in fwd2's exact order: O and the LSE are bitwise equal."""
-    from svdformer_pointsea_amd.attention import AttentionCore
-
-    q, k, v = [t.to(torch.bfloat16) for t in _qkv(B, H, Lq, Lk, E, dev, seed=7)]
-    meta = (H, 1.0 / math.sqrt(E // H), E, False, (0, 0), (1, 0), (2, 0))
-    outs = []
-    for m in ("0", mode):
-        monkeypatch.setenv("PCOPS_FWD3", m)
-        outs.append(AttentionCore.apply(meta, q, k, v))
-    assert torch.equal(outs[0], outs[1])

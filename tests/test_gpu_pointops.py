@@ -33,7 +33,7 @@ FPS_CASES = [
     ("tiny", 2, 37, 20),
     ("wave", 1, 64, 64),
     ("stream", 2, 20000, 300),
-    # work-pruned kernel (2048 < N <= 16384): each points-per-lane instance and its edges
+    # sizes between the step's shapes (register kernel instances and their edges)
     ("p4096", 2, 4096, 1024),
     ("p4097", 1, 4097, 900),
     ("p55", 2, 8192, 2048),
@@ -68,11 +68,11 @@ def test_fps_ties_and_zero_points_bitexact(dev):
 
 
 @pytest.mark.parametrize("kind", ["tiled16384", "zeros8192", "clusters", "line", "all_zero", "gauss16384"])
-def test_fps_pruned_edge_cases_bitexact(dev, kind):
-    """The work-pruned FPS (lanes skipped when their box cannot beat their running
-    distances) on the inputs that stress it: more samples than distinct points
-    (all running distances 0 -> the tie order alone decides), skipped |p|^2 <= 1e-3
-    points, far-apart clusters, a degenerate (flat) box, nothing valid at all."""
+def test_fps_edge_cases_bitexact(dev, kind):
+    """FPS on inputs that stress the tie order and the skip rule: more samples than
+    distinct points (all running distances 0 -> the tie order alone decides),
+    skipped |p|^2 <= 1e-3 points, far-apart clusters, a degenerate (flat) cloud,
+    nothing valid at all."""
     from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
 
     rng = np.random.default_rng(len(kind))
