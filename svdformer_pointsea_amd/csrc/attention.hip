@@ -1022,6 +1022,11 @@ int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, c
   }
   const size_t lds = C::kLds + 4 * kKT * sizeof(float);
   const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
+  if constexpr (D == 128) {
+    // one-pass variants of the D = 128 dK/dV (A/B: PCOPS_DKV128): by 32-query halves, 1 wave per SIMD
+    static const int var = env_int("PCOPS_DKV128", 0);
+    if (var == 1) return launch_dkv2_cfg<128, 4, 3, 1>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+  }
   if (D >= 96 && dkv_split()) {
     // 8 waves per block halve each thread's share of the tile prefetch
     using C8 = Fwd2Cfg<D, 8>;

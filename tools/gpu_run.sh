@@ -82,6 +82,9 @@ run_stage() {
         env $g timeout -k 10 120 python tools/attn_bench.py ${ATTN_SHAPES:-0 1 2 3} >> "$OUT/attn_ab.txt" 2>&1 || return 1
       done ;;
     step_profile) timeout -k 10 400 python tools/step_profile.py --rows 60 > "$OUT/step_ops.txt" 2>&1 ;;
+    gemm_table) GEMM_TABLE=1 timeout -k 10 400 python tools/op_shapes.py x 60 > "$OUT/gemm_table.txt" 2>&1 ;;
+    op_shapes) timeout -k 10 400 python tools/op_shapes.py "${OPS_RE:-^aten::(copy_|cat|fill_|_to_copy)$}" 60 \
+                 > "$OUT/op_shapes.txt" 2>&1 ;;
     glue) timeout -k 10 400 python tools/glue_ops.py > "$OUT/glue_ops.txt" 2>&1 &&
           timeout -k 10 400 python tools/glue_ops.py --model pointsea > "$OUT/glue_ops_pointsea.txt" 2>&1 ;;
     bench_ab)  # quick same-box A/B of the PCN step: one short bench per env group in $BENCH_AB ("A=1;A=0")
