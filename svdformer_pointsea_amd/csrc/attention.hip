@@ -390,11 +390,43 @@ constexpr float kDeferLog2 = PCOPS_DEFER_LOG2;  // forward: rescale only when a 
 // flushed to 0 instead -- invisible in bf16 P (and in any fp32 sum of them).
 __device__ __forceinline__ float exp2_ftz(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// v_max3_f32 as ONE instruction: fmaxf on MFMA results makes the compiler
-// canonicalise each operand first (a v_max x, x per score, IEEE mode)
-__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+// Row max of two 32x32 accumulator tiles as 8 + 7 v_max3_f32 (fmaxf on MFMA
+// results makes the compiler canonicalise each operand first: a v_max x, x
+// per score, IEEE mode).  The operands are MFMA results, and the hazard
+// recognizer does not look inside inline asm: a VALU read of a VGPR written
+// by a 16-pass XDL op needs ~18 wait states on gfx950 that nothing would
+// insert.  Without them v_max3 read accumulators the MFMA had not finished
+// writing (round 3: the 8-wave forward's output differed run to run in the
+// last bf16 bit -- the stale max only shifts the exp reference -- and a max
+// read far too low can overflow exp2 to inf).  Three s_nop 7 (24 wait states)
+// open the first block; the second follows it (volatile order, data chain).
+__device__ __forceinline__ float tile_max16(const f32x16 &a, const f32x16 &b) {
   float r;
-  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm volatile(
+      "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"
+      "v_max3_f32 %0, %1, %2, %3\n\t"
+      "v_max3_f32 %0, %0, %4, %5\n\t"
+      "v_max3_f32 %0, %0, %6, %7\n\t"
+      "v_max3_f32 %0, %0, %8, %9\n\t"
+      "v_max3_f32 %0, %0, %10, %11\n\t"
+      "v_max3_f32 %0, %0, %12, %13\n\t"
+      "v_max3_f32 %0, %0, %14, %15\n\t"
+      "v_max_f32 %0, %0, %16"
+      : "=&v"(r)
+      : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]), "v"(a[2]), "v"(b[2]), "v"(a[3]), "v"(b[3]), "v"(a[4]), "v"(b[4]),
+        "v"(a[5]), "v"(b[5]), "v"(a[6]), "v"(b[6]), "v"(a[7]), "v"(b[7]));
+  asm volatile(
+      "v_max3_f32 %0, %0, %1, %2\n\t"
+      "v_max3_f32 %0, %0, %3, %4\n\t"
+      "v_max3_f32 %0, %0, %5, %6\n\t"
+      "v_max3_f32 %0, %0, %7, %8\n\t"
+      "v_max3_f32 %0, %0, %9, %10\n\t"
+      "v_max3_f32 %0, %0, %11, %12\n\t"
+      "v_max3_f32 %0, %0, %13, %14\n\t"
+      "v_max3_f32 %0, %0, %15, %16"
+      : "+v"(r)
+      : "v"(a[8]), "v"(b[8]), "v"(a[9]), "v"(b[9]), "v"(a[10]), "v"(b[10]), "v"(a[11]), "v"(b[11]), "v"(a[12]),
+        "v"(b[12]), "v"(a[13]), "v"(b[13]), "v"(a[14]), "v"(b[14]), "v"(a[15]), "v"(b[15]));
   return r;
 }
 
@@ -620,9 +652,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
         if (k0 + 32 + acc_row(r, h) >= Lk) X1[r] = -INFINITY;
       }
     }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tmax = max3_raw(tmax, X0[r], X1[r]);
+    float tmax = tile_max16(X0, X1);
     tmax = swap_halves_max(tmax);
     // deferred max (guide T13): while no row's tile max exceeds its running
     // max by more than kDeferLog2 (P <= 2^8), keep m and skip the O rescale;
@@ -942,6 +972,328 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
   if (MODE != 1) store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
 }
 
+// ----------------------------------------------------------------- dK/dV, one pass, software-pipelined (v3)
+// 4 waves x 32 keys per block at one wave per SIMD (D = 128 keeps dK^T, dV^T,
+// the K / V fragments and two half tiles' S / dP live: > 256 registers).  The
+// query stream runs in 32-row half tiles j = 0, 1, 2, ...:
+//   A(j)  S = Q_j K^T, dP = dO_j V^T              (2 D/16 MFMA, rows from LDS)
+//   B(j)  P = exp2(S sl2 - lse2), dS = P (dP - delta), both rounded to bf16 (VALU)
+//   C(j)  dV^T += dO_j^T P,  dK^T += Q_j^T dS      (2 D/16 MFMA, transposed reads)
+// issued as [A(j+1) interleaved with B(j)] then [C(j)]: with no partner wave
+// on the SIMD, the softmax-side VALU of one half fills the MFMA gaps of the
+// next half's products.  The 64-row Q / dO tiles (with their lse / delta)
+// rotate through a 3-slot LDS ring, so one barrier per tile suffices: the slot
+// written before barrier t was last read before barrier t-1.  Per accumulator
+// the MFMA order equals attn_dkv2_kernel MODE 0's, so dK / dV are bitwise the
+// same as that kernel's.
+template <int D>
+__device__ __forceinline__ void v_product_b(f32x16 (&Y)[D / 32], const __bf16 *lds, const bf16x8 (&b)[2]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int row0 = 16 * s + 4 * h + q;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      const int ch = 4 * db + 2 * g + (p >> 1), e = 4 * (p & 1);
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0, ch) + e));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0 + 8, ch) + e));
+      const bf16x8 a = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1,
+                                               2, 3, 4, 5, 6, 7);
+      Y[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[s], Y[db], 0, 0, 0);
+    }
+  }
+#endif
+}
+
+// B(j): the lane's 16 rows are acc_row(r, h) = 8g + 4h + i (r = 4g + i): four
+// float4 LDS reads each of lse2 and delta (cl / cd point at the half's 32 rows),
+// issued in a scheduling region of their own so the VALU groups of the
+// interleaved [A | B] region find their operands ready
+struct RowConsts {
+  float4 l[4], d[4];
+};
+__device__ __forceinline__ void dkv3_rows(RowConsts &rc, const float *cl, const float *cd) {
+  const int h = lane_() >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    rc.l[g] = *reinterpret_cast<const float4 *>(cl + 8 * g + 4 * h);
+    rc.d[g] = *reinterpret_cast<const float4 *>(cd + 8 * g + 4 * h);
+  }
+}
+
+// Instruction order inside the half step.  sched_barrier / sched_group_barrier
+// do not hold here: they are side-effect intrinsics without memory operands,
+// so the IR optimiser moves the (pure) MFMA and VALU work across them (all the
+// fences of a half step ended up together after its last chunk).  An empty
+// volatile asm with "+v" operands does hold: volatile asms keep their order,
+// and an operand redefined by one can only be used after it.  pin() marks the
+// start of a chunk; the chunk's inputs pass through it and its outputs
+// through the next one, so each chunk's VALU and MFMA stay between the two.
+// Diagnostic ablations of the dK/dV v3 loop (tools/dkv3_probe.hip builds; 0 in the
+// product): 1 = B without exp / row constants, 2 = no C MFMAs, 4 = no A MFMAs
+#ifndef PCOPS_DKV3_ABL
+#define PCOPS_DKV3_ABL 0
+#endif
+
+template <typename T>
+__device__ __forceinline__ void pin(T &x) {
+  asm volatile("" : "+v"(x));
+}
+
+// the D/16 row fragments of a 32-row half (k_product's A operands), issued together
+template <int D>
+__device__ __forceinline__ void rows_frag(bf16x8 (&a)[D / 16], const __bf16 *lds) {
+  const int l = lane_(), h = l >> 5, row = l & 31;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) a[s] = *reinterpret_cast<const bf16x8 *>(lds + img_off<D>(row, 2 * s + h));
+}
+
+// the D/16 transposed fragments of a 32-row half (v_product's A operands, [s][db])
+template <int D>
+__device__ __forceinline__ void tr_frag(bf16x8 (&a)[D / 16], const __bf16 *lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int row0 = 16 * s + 4 * h + q;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      const int ch = 4 * db + 2 * g + (p >> 1), e = 4 * (p & 1);
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0, ch) + e));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0 + 8, ch) + e));
+      a[s * (D / 32) + db] =
+          __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+#endif
+}
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float f4_at(const float4 &v, int i) {
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
+// [A(j+1) | B(j)] in D/16 chunks: chunk I = MFMA I of the S chain and of the dP
+// chain, plus B's rows [16 I / (D/16), 16 (I+1) / (D/16)) (whole bf16 pairs:
+// packed words pw / gw[r / 2]).  NEXT = false: B only.  The transposed reads of
+// C(j) are issued after chunk TRI so they land before C starts.
+template <int D, bool NEXT, int I = 0>
+__device__ __forceinline__ void dkv3_ab(f32x16 &Sn, f32x16 &Gn, const bf16x8 (&qa)[D / 16], const bf16x8 (&ga)[D / 16],
+                                        bf16x8 (&kf)[D / 16], bf16x8 (&vf)[D / 16], const f32x16 &S,
+                                        const f32x16 &G, const RowConsts &rc, float sl2, unsigned (&pw)[8],
+                                        unsigned (&gw)[8], bf16x8 (&va)[D / 16], bf16x8 (&ka)[D / 16],
+                                        const __bf16 *hq, const __bf16 *hg) {
+  if constexpr (I < D / 16) {
+    constexpr int R0 = 2 * (8 * I / (D / 16)), R1 = 2 * (8 * (I + 1) / (D / 16));
+    float la[16], da[16];
+#pragma unroll
+    for (int r = R0; r < R1; ++r) {
+      la[r] = f4_at(rc.l[r >> 2], r & 3);
+      da[r] = f4_at(rc.d[r >> 2], r & 3);
+      pin(la[r]);
+      pin(da[r]);
+    }
+    if constexpr (NEXT && !(PCOPS_DKV3_ABL & 4)) {
+      pin(kf[I]);
+      pin(vf[I]);
+      Sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[I], kf[I], Sn, 0, 0, 0);
+      Gn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[I], vf[I], Gn, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = R0; r < R1; r += 2) {
+#if PCOPS_DKV3_ABL & 1
+      const bf16x2 pp = {(__bf16)S[r], (__bf16)S[r + 1]};
+      const bf16x2 gg = {(__bf16)G[r], (__bf16)G[r + 1]};
+#else
+      const float p0 = exp2_ftz(__builtin_fmaf(S[r], sl2, -la[r]));  // 0 for rows beyond Lq (lse = +inf)
+      const float p1 = exp2_ftz(__builtin_fmaf(S[r + 1], sl2, -la[r + 1]));
+      const bf16x2 pp = {(__bf16)p0, (__bf16)p1};
+      const bf16x2 gg = {(__bf16)(p0 * (G[r] - da[r])), (__bf16)(p1 * (G[r + 1] - da[r + 1]))};
+#endif
+      pw[r / 2] = __builtin_bit_cast(unsigned, pp);
+      gw[r / 2] = __builtin_bit_cast(unsigned, gg);
+      pin(pw[r / 2]);
+      pin(gw[r / 2]);
+    }
+    if constexpr (I == D / 32) {
+      tr_frag<D>(va, hg);
+      tr_frag<D>(ka, hq);
+    }
+    dkv3_ab<D, NEXT, I + 1>(Sn, Gn, qa, ga, kf, vf, S, G, rc, sl2, pw, gw, va, ka, hq, hg);
+  }
+}
+
+// C(j): dV^T += dO^T P (va), dK^T += Q^T dS (ka), per accumulator in v_product's order
+template <int D>
+__device__ __forceinline__ void dkv3_c(f32x16 (&Y1)[D / 32], f32x16 (&Y2)[D / 32], const bf16x8 (&va)[D / 16],
+                                       const bf16x8 (&ka)[D / 16], const unsigned (&pw)[8], const unsigned (&gw)[8]) {
+  bf16x8 pb[2], gb[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    pb[s] = __builtin_bit_cast(bf16x8, (u32x4){pw[4 * s], pw[4 * s + 1], pw[4 * s + 2], pw[4 * s + 3]});
+    gb[s] = __builtin_bit_cast(bf16x8, (u32x4){gw[4 * s], gw[4 * s + 1], gw[4 * s + 2], gw[4 * s + 3]});
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      Y1[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s * (D / 32) + db], pb[s], Y1[db], 0, 0, 0);
+      Y2[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s * (D / 32) + db], gb[s], Y2[db], 0, 0, 0);
+    }
+}
+
+template <int D, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dkv3_kernel(
+    const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K, const __bf16 *__restrict__ V,
+    const __bf16 *__restrict__ dO, const float *__restrict__ lse, const float *__restrict__ delta,
+    __bf16 *__restrict__ dK, __bf16 *__restrict__ dV, int Lq, int Lk, float scale, Strides st) {
+  constexpr int NW = 4, RS = Img<D>::RS, TB = kKT * RS;  // TB: elements per tile slot
+  constexpr int kCPT = kKT * D / 8 / (NW * 64);           // 16-B chunks per thread per tile
+  static_assert(kKT * D / 8 % (NW * 64) == 0, "tile chunks must split evenly");
+  extern __shared__ __attribute__((aligned(16))) unsigned char dkv3_smem[];
+  __bf16 *sq = reinterpret_cast<__bf16 *>(dkv3_smem);  // [3][TB]
+  __bf16 *sg = sq + 3 * TB;                             // [3][TB]
+  float *slse = reinterpret_cast<float *>(sg + 3 * TB);  // [3][64]
+  float *sdl = slse + 3 * kKT;                            // [3][64]
+  int rb, bh;
+  xcd_block(rb, bh);
+  const int l = lane_(), h = l >> 5, w = threadIdx.x >> 6;
+  const int k0w = rb * (NW * 32) + w * 32;
+  const int ki = k0w + (l & 31);
+  const bool kv = ki < Lk;
+  bf16x8 kf[D / 16], vf[D / 16];
+  {
+    const __bf16 *kr0 = K + st.k_off(bh) + (long long)(kv ? ki : 0) * st.k_srow + 8 * h;
+    const __bf16 *vr0 = V + st.v_off(bh) + (long long)(kv ? ki : 0) * st.v_srow + 8 * h;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      kf[s] = kv ? *reinterpret_cast<const bf16x8 *>(kr0 + 16 * s) : bf16x8{};
+      vf[s] = kv ? *reinterpret_cast<const bf16x8 *>(vr0 + 16 * s) : bf16x8{};
+    }
+  }
+  const __bf16 *Qb = Q + st.q_off(bh);
+  const __bf16 *Gb = dO + st.o_off(bh);
+  const float *lse_b = lse + (long long)bh * Lq;
+  const float *dl_b = delta + (long long)bh * Lq;
+  const float sl2 = scale * kLog2e;
+  f32x16 Y1[D / 32], Y2[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) {
+    Y1[db] = f32x16{};
+    Y2[db] = f32x16{};
+  }
+  // tile loads: in-tile element offsets are per-thread constants (int: the host
+  // checks 64 row strides fit), the tile base is wave-uniform.  A tile that
+  // runs past Lq (the last one, or one beyond it) reads row Lq-1 in place of
+  // the missing rows: finite values that meet P = 0 there (lse = +inf), so
+  // they add exact zeros to dK / dV
+  bf16x8 qr[kCPT], gr[kCPT];
+  float lr, dr;
+  int qoff[kCPT], goff[kCPT], crow[kCPT];
+#pragma unroll
+  for (int c = 0; c < kCPT; ++c) {
+    const int idx = threadIdx.x + c * NW * 64;
+    crow[c] = idx / (D / 8);
+    qoff[c] = crow[c] * (int)st.q_srow + (idx % (D / 8)) * 8;
+    goff[c] = crow[c] * (int)st.o_srow + (idx % (D / 8)) * 8;
+  }
+  auto load = [&](int t) {
+    const int r0 = t * kKT;
+    if (r0 + kKT <= Lq) {
+      const __bf16 *qb = Qb + (long long)r0 * st.q_srow, *gb = Gb + (long long)r0 * st.o_srow;
+#pragma unroll
+      for (int c = 0; c < kCPT; ++c) {
+        qr[c] = *reinterpret_cast<const bf16x8 *>(qb + qoff[c]);
+        gr[c] = *reinterpret_cast<const bf16x8 *>(gb + goff[c]);
+      }
+      lr = lse_b[r0 + l] * kLog2e;
+      dr = dl_b[r0 + l];
+    } else {
+#pragma unroll
+      for (int c = 0; c < kCPT; ++c) {
+        const int idx = threadIdx.x + c * NW * 64;
+        const long long rr = min(r0 + crow[c], Lq - 1);
+        qr[c] = *reinterpret_cast<const bf16x8 *>(Qb + rr * st.q_srow + (idx % (D / 8)) * 8);
+        gr[c] = *reinterpret_cast<const bf16x8 *>(Gb + rr * st.o_srow + (idx % (D / 8)) * 8);
+      }
+      const int q = r0 + l;
+      const bool ok = q < Lq;
+      const float a = lse_b[ok ? q : Lq - 1], b = dl_b[ok ? q : Lq - 1];
+      lr = ok ? a * kLog2e : INFINITY;
+      dr = ok ? b : 0.f;
+    }
+  };
+  // every wave writes the same 64 lse / delta values (no wave-dependent branch)
+  auto store = [&](int slot) {
+#pragma unroll
+    for (int c = 0; c < kCPT; ++c) {
+      const int idx = threadIdx.x + c * NW * 64;
+      const int row = idx / (D / 8), ch = idx % (D / 8);
+      *reinterpret_cast<bf16x8 *>(sq + slot * TB + img_off<D>(row, ch)) = qr[c];
+      *reinterpret_cast<bf16x8 *>(sg + slot * TB + img_off<D>(row, ch)) = gr[c];
+    }
+    slse[slot * kKT + l] = lr;
+    sdl[slot * kKT + l] = dr;
+  };
+  const int nt = (Lq + kKT - 1) / kKT;
+  load(0);
+  store(0);
+  if (nt > 1) load(1);
+  lds_barrier();
+  f32x16 Sc = f32x16{}, Gc = f32x16{};
+  k_product<D>(Sc, sq, kf);
+  k_product<D>(Gc, sg, vf);
+  int cur = 0, nxt = 1;  // slots of tiles t and t+1
+  // one half step: [A(j+1) | B(j)] then C(j).  hq / hg: this half's Q / dO rows,
+  // nq / ng: the next half's (unused when !NEXT); cl / cd: this half's row constants
+  auto half = [&](auto next_c, const __bf16 *hq, const __bf16 *hg, const __bf16 *nq, const __bf16 *ng,
+                  const float *cl, const float *cd, auto &&mid) {
+    constexpr bool NEXT = decltype(next_c)::value;
+    bf16x8 qa[D / 16], ga[D / 16];
+    if constexpr (NEXT) {
+      rows_frag<D>(qa, nq);
+      rows_frag<D>(ga, ng);
+    }
+    RowConsts rc;
+    dkv3_rows(rc, cl, cd);
+    f32x16 Sn = f32x16{}, Gn = f32x16{};
+    unsigned pw[8], gw[8];
+    bf16x8 va[D / 16], ka[D / 16];
+    dkv3_ab<D, NEXT>(Sn, Gn, qa, ga, kf, vf, Sc, Gc, rc, sl2, pw, gw, va, ka, hq, hg);
+    if constexpr (!(PCOPS_DKV3_ABL & 2)) dkv3_c<D>(Y1, Y2, va, ka, pw, gw);
+    mid();
+    Sc = Sn;
+    Gc = Gn;
+  };
+  const auto none = [] {};
+  int t = 0;
+  for (; t + 1 < nt; ++t) {
+    const __bf16 *cq = sq + cur * TB, *cg = sg + cur * TB;
+    const float *cl = slse + cur * kKT, *cd = sdl + cur * kKT;
+    half(std::true_type{}, cq, cg, cq + 32 * RS, cg + 32 * RS, cl, cd, [&] {
+      store(nxt);
+      load(t + 2);  // past the end: clamped rows, never stored
+    });
+    lds_barrier();
+    half(std::true_type{}, cq + 32 * RS, cg + 32 * RS, sq + nxt * TB, sg + nxt * TB, cl + 32, cd + 32, none);
+    cur = nxt;
+    nxt = nxt == 2 ? 0 : nxt + 1;
+  }
+  {
+    const __bf16 *cq = sq + cur * TB, *cg = sg + cur * TB;
+    const float *cl = slse + cur * kKT, *cd = sdl + cur * kKT;
+    half(std::true_type{}, cq, cg, cq + 32 * RS, cg + 32 * RS, cl, cd, none);
+    half(std::false_type{}, cq + 32 * RS, cg + 32 * RS, cq, cg, cl + 32, cd + 32, none);
+  }
+  store_Y<__bf16, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
+  store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
+}
+
 // D = 64 runs 4-wave blocks at 3 waves per SIMD (the key-half split fits
 // 162 VGPRs): three independent blocks per CU instead of one 8-wave block.
 // PCOPS_DQ_NW4=0 keeps the 8-wave form (A/B).
@@ -1005,10 +1357,42 @@ int launch_dkv2_cfg(const void *q, const void *k, const void *v, const void *dou
   return PCOPS_OK;
 }
 
+template <int D, int OCC>
+int launch_dkv3(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+                void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
+  if ((long long)kKT * (st.q_srow > st.o_srow ? st.q_srow : st.o_srow) >= (1ll << 31)) return PCOPS_ERR_UNSUPPORTED;
+  const size_t lds = 6ull * kKT * Img<D>::RS * sizeof(__bf16) + 6 * kKT * sizeof(float);
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv3_kernel<D, OCC>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
+  const dim3 grid((Lk + 127) / 128, BH);
+  hipLaunchKernelGGL((attn_dkv3_kernel<D, OCC>), grid, dim3(256), lds, s, (const __bf16 *)q, (const __bf16 *)k,
+                     (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk, (__bf16 *)dv, Lq, Lk, scale,
+                     st);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+// dK/dV pass selection: the pipelined one-pass v3 kernel for D = 96 / 128 (bitwise the
+// split v2 passes' results; A/B at the PCN shapes: 2048^2 hd128 1.51 -> 1.38 ms, 512^2
+// hd96 0.105 -> 0.089 ms).  D = 64 keeps the 8-wave v2 pass (v3 at one wave per SIMD:
+// 0.70 -> 1.0 ms).  PCOPS_DKV3: 0 = never v3, 1 = v3 for every D >= 64 (A/B runs).
+int dkv3_mode() {
+  static const int v = env_int("PCOPS_DKV3", -1);
+  return v;
+}
+
 template <int D, int NW>
 int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                 void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
   using C = Fwd2Cfg<D, NW>;
+  if constexpr (D >= 64) {
+    const int m3 = dkv3_mode();
+    if (m3 == 1 || (m3 < 0 && D >= 96)) {
+      const int rc = launch_dkv3<D, 1>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      if (rc != PCOPS_ERR_UNSUPPORTED) return rc;  // strides too large for its 32-bit tile offsets: v2 below
+    }
+  }
   if constexpr (D == 64 && NW == 8) {
     // occupancy variants of the long-sequence D = 64 pass (A/B: PCOPS_DKV64)
     static const int var = env_int("PCOPS_DKV64", 0);

@@ -100,6 +100,28 @@ def test_core_bf16(dev, B, H, Lq, Lk, E):
         assert rel < 3e-2, rel
 
 
+@pytest.mark.parametrize("B,H,Lq,Lk,E", [(2, 8, 2048, 2048, 512), (2, 8, 2048, 2048, 1024), (2, 4, 130, 129, 128),
+                                         (1, 8, 333, 250, 1024)])
+def test_core_bf16_run_to_run_bitwise(dev, B, H, Lq, Lk, E):
+    """The bf16 kernels are deterministic: four forward + backward passes on the same
+    inputs agree bit for bit (round 3: the 8-wave forward read MFMA accumulators
+    through an inline-asm v_max3 before the MFMA had written them -- no hazard wait
+    states are inserted for asm -- and its output moved in the last bit run to run)."""
+    from svdformer_pointsea_amd.attention import attention_core
+
+    q, k, v = [t.to(torch.bfloat16) for t in _qkv(B, H, Lq, Lk, E, dev, seed=3)]
+    g = torch.randn(Lq, B, E, generator=torch.Generator().manual_seed(8)).to(dev, torch.bfloat16)
+    runs = []
+    for _ in range(4):
+        qs, ks, vs = [t.clone().requires_grad_(True) for t in (q, k, v)]
+        o = attention_core(qs, ks, vs, H)
+        o.backward(g)
+        runs.append((o.detach(), qs.grad, ks.grad, vs.grad))
+    for r in runs[1:]:
+        for name, a, b in zip(("o", "dq", "dk", "dv"), runs[0], r):
+            assert torch.equal(a, b), name
+
+
 def _nrand(seed, *shape):
     return torch.from_numpy(np.random.default_rng(seed).standard_normal(shape).astype(np.float32))
 

@@ -102,6 +102,16 @@ run_stage() {
         echo "== $g" >> "$OUT/fps_bench.txt"
         env $g timeout -k 10 120 python tools/fps_bench.py >> "$OUT/fps_bench.txt" 2>&1 || return 1
       done ;;
+    attn_var)  # bitwise / float64 check of an attention variant: default vs each env group in $ATTN_VAR
+      timeout -k 10 300 python tools/attn_variant.py dump "$OUT/attn_var_base.pt" > "$OUT/attn_var.txt" 2>&1 || return 1
+      IFS=';' read -ra groups <<< "${ATTN_VAR:?set ATTN_VAR}"
+      for g in "${groups[@]}"; do
+        echo "== $g" >> "$OUT/attn_var.txt"
+        env $g timeout -k 10 300 python tools/attn_variant.py dump "$OUT/attn_var_x.pt" >> "$OUT/attn_var.txt" 2>&1 || return 1
+        python tools/attn_variant.py cmp "$OUT/attn_var_base.pt" "$OUT/attn_var_x.pt" >> "$OUT/attn_var.txt" 2>&1
+      done
+      rm -f "$OUT"/attn_var_*.pt ;;
+    attn_det) timeout -k 10 300 python tools/attn_determinism.py > "$OUT/attn_det.txt" 2>&1 ;;
     attn_err) timeout -k 10 300 python tools/attn_err.py > "$OUT/attn_err.jsonl" 2>&1 ;;
     chamfer) timeout -k 10 120 python tools/microbench.py > "$OUT/chamfer_bench.txt" 2>&1 ;;
     *) echo "unknown stage $1"; return 2 ;;
