@@ -20,6 +20,7 @@ win = [e for e in ev[a + 1:b] if e[0] >= t0 and e[1] <= t1]
 
 
 def short(n):
+    n = n.replace("(anonymous namespace)::", "")
     m = re.search(r"([A-Za-z_]\w*)<([^()]*)>\(", n)
     if m and "at::native" not in n:
         return f"{m.group(1)}<{m.group(2)}>"
