@@ -70,7 +70,13 @@ def _wgrad(g2, x2, wdt):
     if not _WGRAD_SPLITK:
         return (g2.t() @ x2).to(wdt)
     S = 16 if Cout * Cin <= (2 << 20) else 4
-    while S > 1 and (T % S or T // S < 2048):
+    if Cout * Cin < (1 << 18) and _WGRAD_SMALL:
+        # small outputs: 16 slices gave hipBLASLt 16 workgroups for the whole GEMM
+        # (3 x 64 / 64 x 32 / 128 x 128 over 0.5-1 M tokens ran at 1.6-109 TFLOP/s);
+        # about 2^22 output elements over all slices fill the chip
+        S = max(S, min(512, (1 << 22) // (Cout * Cin)))
+        S = 1 << (S.bit_length() - 1)
+    while S > 1 and (T % S or T // S < (1024 if S > 16 else 2048)):
         S //= 2
     if S == 1 or g2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16:
         return (g2.t() @ x2).to(wdt)
@@ -91,9 +97,10 @@ class _Linear(Function):
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, b_dtype=None):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        ctx.b_dtype = b_dtype   # the bias's own dtype (custom_fwd hands forward the bf16 cast)
         # on a side stream: GEMMs without stream-K (forward here, backward on
         # the same stream later -- autograd replays the forward's streams)
         ctx.side = _lib.on_side_stream()
@@ -116,8 +123,10 @@ class _Linear(Function):
             # a LayerNorm backward that consumed this output may have summed g
             # already (pcops_layernorm_bwd_colsum, attached to g); else one colsum
             pre = _take_sum(g)
-            gb = pre if pre is not None else colsum(g2.contiguous())
-        return gx, gw, gb
+            gb = pre if pre is not None else colsum(g2.contiguous(), out_dtype=ctx.b_dtype)
+        if gb is not None and ctx.b_dtype is not None and gb.dtype != ctx.b_dtype:
+            gb = gb.to(ctx.b_dtype)
+        return gx, gw, gb, None
 
 
 _PRESUM = "_pcops_bias_colsum"   # attribute a gradient tensor carries when its column sum is known
@@ -189,12 +198,16 @@ def linear(x, w, b=None):
     goes through _lib.no_stream_k."""
     if _lib.on_side_stream() and x.is_cuda:
         if torch.is_grad_enabled() and (w.requires_grad or x.requires_grad):
-            return _Linear.apply(x, w, b)      # both directions without stream-K
+            return _Linear.apply(x, w, b, _bdt(b))      # both directions without stream-K
         with _lib.no_stream_k():
             return F.linear(x, w, b)
     if not (x.is_cuda and torch.is_grad_enabled() and w.requires_grad and x.numel() // x.shape[-1] >= 8192):
         return F.linear(x, w, b)
-    return _Linear.apply(x, w, b)
+    return _Linear.apply(x, w, b, _bdt(b))
+
+
+def _bdt(b):
+    return b.dtype if b is not None else None
 
 
 # ------------------------------------------------------------------ attention core
@@ -318,8 +331,12 @@ class MultiheadAttention(nn.Module):
             nn.init.constant_(self.out_proj.bias, 0.0)
 
     def _proj(self, x, r0, r1):
-        b = None if self.in_proj_bias is None else self.in_proj_bias[r0:r1]
-        return linear(x, self.in_proj_weight[r0:r1], b)
+        # the whole packed weight unsliced: a [0:3E] slice cost a SliceBackward (a
+        # full-size zero fill + copy) per weight and bias every step
+        full = (r0, r1) == (0, self.in_proj_weight.shape[0])
+        w = self.in_proj_weight if full else self.in_proj_weight[r0:r1]
+        b = None if self.in_proj_bias is None else (self.in_proj_bias if full else self.in_proj_bias[r0:r1])
+        return linear(x, w, b)
 
     def forward(self, query, key, value, need_weights=True):
         E, H = self.embed_dim, self.num_heads
@@ -602,6 +619,7 @@ _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
 _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
 _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
 _WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switch: split-K weight gradients
+_WGRAD_SMALL = os.environ.get("PCOPS_WGRAD_SMALL", "1") != "0"    # A/B switch: more split-K slices for small weights
 _PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
 _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnostic: fused sums in side-stream blocks too
 # linear11's bias sum inside the GELU backward (A/B switch); the sum reaches the

@@ -656,7 +656,7 @@ def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
     x = torch.randn(4, 64, 2048, device=dev)            # 8192 tokens: the _Linear path
     calls = []
     real = A.colsum
-    monkeypatch.setattr(A, "colsum", lambda g: calls.append(g.shape) or real(g))
+    monkeypatch.setattr(A, "colsum", lambda g, **kw: calls.append(g.shape) or real(g, **kw))
 
     monkeypatch.setattr(A, "_GELU_SUM", True)
 
