@@ -256,6 +256,140 @@ __global__ __launch_bounds__(256) void pcsa_bwd_wave_kernel(const void *__restri
   }
 }
 
+// ---- MFMA form for bf16 features, K = 16 (the models' PCSA: C = 128 / 256, K = 16).
+// Per (b, s) patch the chain is two 16x16 matrix products per 16-channel block,
+// on v_mfma_f32_16x16x16_bf16 with the rounding the reference's autocast chain
+// applies (model_utils.py:413-430 under bf16 autocast: spec = bf16(x @ D^T),
+// bf16(spec * gates), out = bf16(spec_g @ D)):
+//   Y = D X_blk (fp32 accumulate) -> Z = bf16(bf16(Y) g) -> O = D^T Z -> bf16.
+// Operand maps (16x16x16 bf16): lane l holds A[l&15][4(l>>4)+j], B[4(l>>4)+j][l&15]
+// and the result D[4(l>>4)+j][l&15], j = 0..3 -- so the accumulator of the
+// first product IS the B operand of the second (no lane movement).  X's B
+// fragments come from an LDS image of the patch by ds_read_b64_tr_b16 (lane
+// 4r+c of a 16-lane group addresses row r, columns 4c..4c+3 of its 4x16 block
+// and receives one column); rows padded by 32 B so a 32-lane half's 8 rows hit
+// 32 distinct banks.  One wave per patch, 4 patches per block.
+// Backward: u = D dout, v = D x (both rounded to bf16 as the reference stores
+// them), dgates[k] = sum_c bf16(u v) (the RepeatBackward sum, fp32), dx = D^T bf16(u g).
+typedef short pc_short4 __attribute__((ext_vector_type(4)));
+typedef float pc_f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 pc_bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 pc_bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bfr(float v) { return (float)(__bf16)v; }  // round to bf16 and back
+
+__device__ __forceinline__ pc_short4 bf4(float a, float b, float c, float d) {
+  const pc_bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  return __builtin_bit_cast(pc_short4, v);
+}
+
+// stage the 16 x C bf16 patch at src (rows C apart) into a padded LDS image
+template <int C>
+__device__ __forceinline__ void pcsa_stage(__bf16 *img, const __bf16 *src, int lane) {
+  constexpr int RS = C + 16;
+#pragma unroll
+  for (int t = lane; t < 2 * C; t += 64) {  // 16 rows x C/8 chunks of 8
+    const int row = t / (C / 8), ch = t % (C / 8);
+    *reinterpret_cast<pc_bf16x8 *>(img + row * RS + ch * 8) = *reinterpret_cast<const pc_bf16x8 *>(src + row * C + ch * 8);
+  }
+}
+
+// B fragment of channel block cb: rows 4(l>>4)..+3, column 16 cb + (l&15)
+template <int C>
+__device__ __forceinline__ pc_short4 pcsa_bfrag(const __bf16 *img, int lane, int cb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int RS = C + 16;
+  typedef __attribute__((address_space(3))) pc_short4 lds_s4;
+  const int g = lane >> 4, i = lane & 15;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(img + (4 * g + (i >> 2)) * RS + 16 * cb + 4 * (i & 3)));
+#else
+  return pc_short4{};
+#endif
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void pcsa_fwd_mfma_kernel(const __bf16 *__restrict__ x, const void *__restrict__ gates,
+                                                            int gdt, const float *__restrict__ basis, int patches,
+                                                            __bf16 *__restrict__ out) {
+  constexpr int K = 16, RS = C + 16;
+  __shared__ __attribute__((aligned(16))) __bf16 simg[4][K * RS];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, q = l >> 4, c = l & 15;
+  const long long p = (long long)blockIdx.x * 4 + w;
+  if (p >= patches) return;  // whole waves only; no block barrier below
+  const pc_short4 da = bf4(basis[c * K + 4 * q], basis[c * K + 4 * q + 1], basis[c * K + 4 * q + 2],
+                           basis[c * K + 4 * q + 3]);                            // D[c][4q + j]
+  const pc_short4 dt = bf4(basis[(4 * q) * K + c], basis[(4 * q + 1) * K + c], basis[(4 * q + 2) * K + c],
+                           basis[(4 * q + 3) * K + c]);                          // D[4q + j][c]
+  float g[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = ldv(gates, gdt, p * K + 4 * q + i);
+  __bf16 *img = simg[w];
+  pcsa_stage<C>(img, x + p * K * C, l);
+  __bf16 *ob = out + p * K * C;
+#pragma unroll
+  for (int cb = 0; cb < C / 16; ++cb) {
+    const pc_f32x4 y = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, pcsa_bfrag<C>(img, l, cb), pc_f32x4{}, 0, 0, 0);
+    const pc_short4 z = bf4(bfr(y[0]) * g[0], bfr(y[1]) * g[1], bfr(y[2]) * g[2], bfr(y[3]) * g[3]);
+    const pc_f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(dt, z, pc_f32x4{}, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ob[(4 * q + i) * C + 16 * cb + c] = (__bf16)o[i];
+  }
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void pcsa_bwd_mfma_kernel(const __bf16 *__restrict__ x, const __bf16 *__restrict__ dout,
+                                                            const void *__restrict__ gates, int gdt,
+                                                            const float *__restrict__ basis, int patches,
+                                                            __bf16 *__restrict__ dx, void *__restrict__ dgates) {
+  constexpr int K = 16, RS = C + 16;
+  __shared__ __attribute__((aligned(16))) __bf16 simg[4][2][K * RS];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, q = l >> 4, c = l & 15;
+  const long long p = (long long)blockIdx.x * 4 + w;
+  if (p >= patches) return;
+  const pc_short4 da = bf4(basis[c * K + 4 * q], basis[c * K + 4 * q + 1], basis[c * K + 4 * q + 2],
+                           basis[c * K + 4 * q + 3]);
+  const pc_short4 dt = bf4(basis[(4 * q) * K + c], basis[(4 * q + 1) * K + c], basis[(4 * q + 2) * K + c],
+                           basis[(4 * q + 3) * K + c]);
+  float g[4], dg[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = ldv(gates, gdt, p * K + 4 * q + i);
+  __bf16 *ix = simg[w][0], *id = simg[w][1];
+  pcsa_stage<C>(ix, x + p * K * C, l);
+  pcsa_stage<C>(id, dout + p * K * C, l);
+  __bf16 *ob = dx + p * K * C;
+#pragma unroll
+  for (int cb = 0; cb < C / 16; ++cb) {
+    const pc_f32x4 u = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, pcsa_bfrag<C>(id, l, cb), pc_f32x4{}, 0, 0, 0);
+    const pc_f32x4 v = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, pcsa_bfrag<C>(ix, l, cb), pc_f32x4{}, 0, 0, 0);
+    float ub[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ub[i] = bfr(u[i]);
+      dg[i] += bfr(ub[i] * bfr(v[i]));
+    }
+    const pc_short4 s = bf4(ub[0] * g[0], ub[1] * g[1], ub[2] * g[2], ub[3] * g[3]);
+    const pc_f32x4 o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(dt, s, pc_f32x4{}, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ob[(4 * q + i) * C + 16 * cb + c] = (__bf16)o[i];
+  }
+  // sum over the 16 channel lanes of each 16-lane group (rows 4q .. 4q+3)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) dg[i] += __shfl_xor(dg[i], o, 64);
+    if (c == 0) stv(dgates, gdt, p * K + 4 * q + i, dg[i]);
+  }
+}
+
+// A/B: PCOPS_PCSA_MFMA=0 keeps the fp32-VALU kernels for bf16 features too
+bool pcsa_mfma(int K, int C, int xdt) {
+  static const bool off = [] {
+    const char *e = getenv("PCOPS_PCSA_MFMA");
+    return e && e[0] == '0';
+  }();
+  return !off && xdt == 1 && K == 16 && (C == 64 || C == 128 || C == 256);
+}
+
 // A/B: PCOPS_PCSA_V1=1 keeps the block-per-patch kernels
 bool pcsa_wave(int K, int C) {
   static const bool v1 = [] {
@@ -273,6 +407,18 @@ extern "C" int pcops_pcsa_forward(const void *x, int x_dtype, const void *gates,
   if (patches == 0) return PCOPS_OK;
   if (!x || !gates || !basis || !out || (x_dtype & ~1) || (gates_dtype & ~1)) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  if (pcsa_mfma(K, C, x_dtype)) {
+    const dim3 grid((patches + 3) / 4);
+#define PCSA_FM(CC)                                                                                             \
+  if (C == CC) {                                                                                              \
+    hipLaunchKernelGGL(pcsa_fwd_mfma_kernel<CC>, grid, dim3(256), 0, s, (const __bf16 *)x, gates, gates_dtype, \
+                       basis, patches, (__bf16 *)out);                                                          \
+    PC_CHECK_LAUNCH();                                                                                        \
+    return PCOPS_OK;                                                                                          \
+  }
+    PCSA_FM(64) PCSA_FM(128) PCSA_FM(256)
+#undef PCSA_FM
+  }
   if (pcsa_wave(K, C) && C <= 128) {  // C = 256 forward: the block form measured faster (0.110 vs 0.133 ms)
     const dim3 grid((patches + 3) / 4);
 #define PCSA_FW(KK, CC)                                                                                        \
@@ -305,6 +451,18 @@ extern "C" int pcops_pcsa_backward(const void *x, int x_dtype, const void *dout,
   if (!x || !dout || !gates || !basis || !dx || !dgates || (x_dtype & ~1) || (dout_dtype & ~1) || (gates_dtype & ~1))
     return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  if (pcsa_mfma(K, C, x_dtype) && dout_dtype == 1) {
+    const dim3 grid((patches + 3) / 4);
+#define PCSA_BM(CC)                                                                                              \
+  if (C == CC) {                                                                                               \
+    hipLaunchKernelGGL(pcsa_bwd_mfma_kernel<CC>, grid, dim3(256), 0, s, (const __bf16 *)x, (const __bf16 *)dout, \
+                       gates, gates_dtype, basis, patches, (__bf16 *)dx, dgates);                              \
+    PC_CHECK_LAUNCH();                                                                                         \
+    return PCOPS_OK;                                                                                           \
+  }
+    PCSA_BM(64) PCSA_BM(128) PCSA_BM(256)
+#undef PCSA_BM
+  }
   if (pcsa_wave(K, C)) {
     const dim3 grid((patches + 3) / 4);
 #define PCSA_BW(KK, CC)                                                                                        \

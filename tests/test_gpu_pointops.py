@@ -475,7 +475,7 @@ def test_pcviews_real_golden(dev):
 
 @pytest.mark.parametrize("dtype,K,C", [(torch.float32, 16, 128), (torch.float32, 16, 256), (torch.bfloat16, 16, 128),
                                        (torch.bfloat16, 16, 256), (torch.float32, 4, 96), (torch.bfloat16, 8, 64),
-                                       (torch.float32, 8, 64)])
+                                       (torch.float32, 8, 64), (torch.bfloat16, 16, 64)])
 def test_pcsa_kernel_matches_torch_chain(dev, dtype, K, C):
     """PCSA (model_utils.py:408-430): the libpcops patch kernel vs the
     reference's permute / DCT matmul / gate / IDCT matmul chain, fwd + bwd."""
