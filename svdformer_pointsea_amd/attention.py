@@ -73,8 +73,9 @@ def _wgrad(g2, x2, wdt):
     if Cout * Cin < (1 << 18) and _WGRAD_SMALL:
         # small outputs: 16 slices gave hipBLASLt 16 workgroups for the whole GEMM
         # (3 x 64 / 64 x 32 / 128 x 128 over 0.5-1 M tokens ran at 1.6-109 TFLOP/s);
-        # about 2^22 output elements over all slices fill the chip
-        S = max(S, min(512, (1 << 22) // (Cout * Cin)))
+        # about 2^20 partial elements over all slices: enough workgroups, and the
+        # fixed-order sum of the slices (pcops_sum_rows) stays a few MB
+        S = max(S, min(512, (1 << 20) // (Cout * Cin)))
         S = 1 << (S.bit_length() - 1)
     while S > 1 and (T % S or T // S < (1024 if S > 16 else 2048)):
         S //= 2
