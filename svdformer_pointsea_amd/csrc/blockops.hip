@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a,
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += ok ? x[i].v[k] : 0.f;
   }
-  const float mean = wave_sum_f32(s) / (float)C;
+  const float mean = wave_sum_f32_dpp(s) / (float)C;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < CH; ++i) {
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a,
       q = __builtin_fmaf(d, d, q);
     }
   }
-  const float rstd = 1.f / sqrtf(wave_sum_f32(q) / (float)C + eps);
+  const float rstd = 1.f / sqrtf(wave_sum_f32_dpp(q) / (float)C + eps);
 #pragma unroll
   for (int i = 0; i < CH; ++i) {
     const int ch = lane + 64 * i;
@@ -239,8 +239,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
         sgx = __builtin_fmaf(g, xh[i].v[k], sgx);
       }
     }
-    const float mg = wave_sum_f32(sg) / (float)C;
-    const float mgx = wave_sum_f32(sgx) / (float)C;
+    const float mg = wave_sum_f32_dpp(sg) / (float)C;
+    const float mgx = wave_sum_f32_dpp(sgx) / (float)C;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int ch = lane + 64 * i;

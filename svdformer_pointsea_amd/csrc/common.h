@@ -47,6 +47,28 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
   return v;
 }
 
+// Wave sum without LDS: __shfl_xor lowers to ds_bpermute_b32, six dependent
+// LDS round trips (each behind an lgkmcnt(0) wait) per sum.  Here four DPP
+// steps inside each 16-lane row (xor 1, xor 2, half-row mirror, row mirror)
+// and the gfx950 row swaps (v_permlane16_swap: rows 0<->1, 2<->3;
+// v_permlane32_swap: halves) -- all VALU.  Every lane ends with the same
+// bits (each step adds a commutative pair).  The association differs from
+// wave_sum_f32's, so results differ from it in the last bits.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add_f32(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_f32_dpp(float v) {
+  v = dpp_add_f32<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = dpp_add_f32<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = dpp_add_f32<0x141>(v);  // row_half_mirror
+  v = dpp_add_f32<0x140>(v);  // row_mirror
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
 // ---- DPP wave reductions (no LDS traffic; result broadcast via readlane) ----
 // quad_perm [1,0,3,2] / [2,3,0,1], row_half_mirror, row_mirror give every lane
 // its 16-lane row's value; row_bcast15 / row_bcast31 (GFX9 DPP, available on
