@@ -91,7 +91,12 @@ def synth_pcn(B, seed, device):
     """PCN-shaped synthetic batch: gt (B,16384,3) on random rotated
     ellipsoid surfaces inside the unit cube; partial (B,2048,3) = the half
     facing a random view, resampled to 2048 with replacement (the PCN
-    loader's RandomSamplePoints)."""
+    loader's RandomSamplePoints).  The partial points are a second, independent
+    sampling of the same surface (PCN's partials are separate renders, never
+    gt's own points): with partial a subset of gt, a partial point that FPS
+    keeps in the coarse prediction can land exactly on a gt_c point, and the
+    sqrt-Chamfer gradient there is 0 * inf = NaN (it made some training runs
+    diverge after a few steps, depending on the trajectory)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     d = torch.randn(B, 16384, 3, generator=g)
     d = d / d.norm(dim=-1, keepdim=True)
@@ -99,9 +104,12 @@ def synth_pcn(B, seed, device):
     q, _ = torch.linalg.qr(torch.randn(B, 3, 3, generator=g))
     gt = torch.bmm(d * axes, q)
     view = torch.randn(B, 3, generator=g)
+    d2 = torch.randn(B, 16384, 3, generator=g)
+    d2 = d2 / d2.norm(dim=-1, keepdim=True)
+    scan = torch.bmm(d2 * axes, q)
     partial = torch.empty(B, 2048, 3)
     for b in range(B):
-        vis = gt[b][(d[b] @ (view[b] / view[b].norm())) > 0]
+        vis = scan[b][(d2[b] @ (view[b] / view[b].norm())) > 0]
         pick = torch.randint(0, vis.shape[0], (2048,), generator=g)
         partial[b] = vis[pick]
     return partial.contiguous().to(device), gt.contiguous().to(device)

@@ -75,7 +75,7 @@ def _wgrad(g2, x2, wdt):
         # (3 x 64 / 64 x 32 / 128 x 128 over 0.5-1 M tokens ran at 1.6-109 TFLOP/s);
         # about 2^20 partial elements over all slices: enough workgroups, and the
         # fixed-order sum of the slices (pcops_sum_rows) stays a few MB
-        S = max(S, min(512, (1 << 20) // (Cout * Cin)))
+        S = max(S, min(512, (1 << _WGRAD_SMALL_LOG2) // (Cout * Cin)))
         S = 1 << (S.bit_length() - 1)
     while S > 1 and (T % S or T // S < (1024 if S > 16 else 2048)):
         S //= 2
@@ -621,6 +621,7 @@ _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch:
 _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
 _WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switch: split-K weight gradients
 _WGRAD_SMALL = os.environ.get("PCOPS_WGRAD_SMALL", "1") != "0"    # A/B switch: more split-K slices for small weights
+_WGRAD_SMALL_LOG2 = int(os.environ.get("PCOPS_WGRAD_SMALL_LOG2", "20"))  # partial elements aimed at (log2)
 _PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
 _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnostic: fused sums in side-stream blocks too
 # linear11's bias sum inside the GELU backward (A/B switch); the sum reaches the

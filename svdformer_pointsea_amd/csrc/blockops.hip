@@ -566,6 +566,53 @@ __global__ __launch_bounds__(256) void sum_rows_kernel(const float *__restrict__
   }
 }
 
+// Many rows over few columns (the split-K weight gradient of a small weight: S = 64..512 slices of
+// 192..16K values): a block takes 16 column quads x 16 row slices; slice sl sums rows sl, sl + 16,
+// ... with eight loads in flight, then the 16 slices are added in slice order through LDS -- a
+// fixed order, so still deterministic.  One thread per column quad walking all S rows (the plain
+// kernel) was latency-bound there: 512 dependent-in-groups-of-4 loads in 1..16 blocks.
+__global__ __launch_bounds__(256) void sum_rows_sliced_kernel(const float *__restrict__ part, int S, long long n4,
+                                                              long long N, void *__restrict__ out, int odt) {
+  __shared__ float4 red[16][16];
+  const int cq = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const long long i = (long long)blockIdx.x * 16 + cq;
+  float4 a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    int r = sl;
+    for (; r + 7 * 16 < S; r += 8 * 16)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 v = *reinterpret_cast<const float4 *>(part + (long long)(r + 16 * j) * N + 4 * i);
+        a[j].x += v.x, a[j].y += v.y, a[j].z += v.z, a[j].w += v.w;
+      }
+    for (; r < S; r += 16) {
+      const float4 v = *reinterpret_cast<const float4 *>(part + (long long)r * N + 4 * i);
+      a[0].x += v.x, a[0].y += v.y, a[0].z += v.z, a[0].w += v.w;
+    }
+  }
+#pragma unroll
+  for (int j = 1; j < 8; ++j) a[0].x += a[j].x, a[0].y += a[j].y, a[0].z += a[j].z, a[0].w += a[j].w;
+  red[sl][cq] = a[0];
+  __syncthreads();
+  if (sl != 0 || i >= n4) return;
+  float4 acc = red[0][cq];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) {
+    const float4 v = red[j][cq];
+    acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+  }
+  if (odt == 0) {
+    *reinterpret_cast<float4 *>(reinterpret_cast<float *>(out) + 4 * i) = acc;
+  } else {
+    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+    bf16x4_t o;
+    o[0] = (__bf16)acc.x, o[1] = (__bf16)acc.y, o[2] = (__bf16)acc.z, o[3] = (__bf16)acc.w;
+    *reinterpret_cast<bf16x4_t *>(reinterpret_cast<__bf16 *>(out) + 4 * i) = o;
+  }
+}
+
 // stage 1 of a long row sum: part2[y][i] = sum_{s = y, y + P, ...} part[s][i] (grid.y = P slices),
 // eight independent loads in flight per thread (a single pass over 512 rows was latency-bound)
 __global__ __launch_bounds__(256) void sum_rows_split_kernel(const float *__restrict__ part, int S, long long n4,
@@ -887,8 +934,13 @@ extern "C" int pcops_sum_rows(const float *part, int S, long long N, void *out, 
   if (N % 4) return PCOPS_ERR_UNSUPPORTED;
   if (!part || !out) return PCOPS_ERR_INVALID;
   const long long n4 = N / 4;
-  hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, part, S,
-                     n4, N, out, out_dtype);
+  static const bool sliced = colsum_env("PCOPS_SUMROWS_SLICED", 1) != 0;
+  if (S >= 32 && sliced)
+    hipLaunchKernelGGL(sum_rows_sliced_kernel, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, (hipStream_t)stream,
+                       part, S, n4, N, out, out_dtype);
+  else
+    hipLaunchKernelGGL(sum_rows_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, part,
+                       S, n4, N, out, out_dtype);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

@@ -362,7 +362,9 @@ def test_colsum_matches_float64(dev, rows, C, dtype):
 
 @pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("T,Cout,Cin", [(65536, 512, 512), (16384, 768, 256), (8192, 1024, 512),
-                                        (32 * 2048 * 16, 32, 6), (1000, 64, 6)])
+                                        (32 * 2048 * 16, 32, 6), (1000, 64, 6),
+                                        # small weights: up to 512 slices, summed by the sliced pcops_sum_rows
+                                        (32 * 16384, 3, 64), (1 << 20, 64, 32), (32 * 16384, 128, 128)])
 def test_split_k_wgrad_matches_float64(dev, wdt, T, Cout, Cin):
     """The blocks' split-K weight gradient (bmm partials + pcops_sum_rows: fixed-order sum,
     one rounding) -- and EdgeConv's 6-channel one (pcops_wgrad_skinny) -- vs float64 g^T x:
@@ -677,6 +679,58 @@ def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
         # separate colsum rounds its result to the gradient's dtype
         tol = dict(rtol=1e-2, atol=1e-5) if amp else dict(rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(g_fus[n], g_ref[n], **tol, msg=n)
+
+
+@pytest.mark.parametrize("S", [16, 32, 64, 128, 256, 512])
+@pytest.mark.parametrize("N", [192, 2048, 8192, 16384, 32768, 65536, 131072, 1 << 20])
+def test_sum_rows_matches_float64(dev, S, N):
+    """pcops_sum_rows (the split-K partial sum: plain form for S < 32, sliced form above):
+    every (slices, columns) combination the weight gradients produce, fp32 and bf16 out."""
+    from svdformer_pointsea_amd._lib import call, lib, ptr, stream_of
+
+    part = torch.randn(S, N, device=dev, generator=torch.Generator(device=dev).manual_seed(S * 7 + N))
+    ref = part.double().sum(0)
+    for odt, dt in ((0, torch.float32), (1, torch.bfloat16)):
+        out = torch.empty(N, dtype=dt, device=dev)
+        call("sum_rows", lib().pcops_sum_rows, ptr(part), S, N, ptr(out), odt, stream_of(part))
+        torch.cuda.synchronize()
+        tol = 1e-5 * S ** 0.5 + (2 ** -8 * ref.abs() if odt else 0)
+        assert bool(((out.double() - ref).abs() <= tol).all()), (odt, float((out.double() - ref).abs().max()))
+
+
+@pytest.mark.parametrize("S,N", [(64, 16384), (128, 8192), (512, 192), (32, 32768)])
+def test_sum_rows_graph_replay(dev, S, N):
+    """The split-K partial sum captured in a HIP graph with the bmm that produces its input
+    (as the bench step does): every replay equals the eager result bitwise."""
+    from svdformer_pointsea_amd._lib import call, lib, ptr, stream_of
+
+    T = S * 1024
+    Cin = 64
+    Cout = N // Cin
+    gen = torch.Generator(device=dev).manual_seed(S + N)
+    g2 = torch.randn(T, Cout, device=dev, generator=gen).to(torch.bfloat16)
+    x2 = torch.randn(T, Cin, device=dev, generator=gen).to(torch.bfloat16)
+
+    def run(out):
+        part = torch.bmm(g2.view(S, T // S, Cout).transpose(1, 2), x2.view(S, T // S, Cin), out_dtype=torch.float32)
+        call("sum_rows", lib().pcops_sum_rows, ptr(part), S, N, ptr(out), 1, stream_of(part))
+
+    eager = torch.empty(N, dtype=torch.bfloat16, device=dev)
+    run(eager)
+    out = torch.empty_like(eager)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        run(out)
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        run(out)
+    for _ in range(5):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
 
 
 @pytest.mark.parametrize("n", [8, 1000, 1003, 1 << 20])
