@@ -142,7 +142,13 @@ def synth_55(B, seed, device, n_gt=8192):
 
 
 # ------------------------------------------------------------------ roofline model
-ATTN_ARGS = {"attention forward": 5, "attention bwd dq": 7, "attention bwd dkv": 7}  # position of B
+# attention calls: B is followed by H, Lq, Lk, D, scale, dtype, 12 strides and 1 (forward) or 3 trailing
+# args, so its position counts from the end (the *_colsum entries carry extra pointers before B)
+ATTN_ARGS = {"attention forward": 20, "attention bwd dq": 22, "attention bwd dkv": 22}
+
+
+def _attn_b(name, a):
+    return len(a) - ATTN_ARGS[name]
 
 
 def kernel_work(name, a):
@@ -160,7 +166,7 @@ def kernel_work(name, a):
       glue kernels    bytes that must cross HBM once (each branch states its count)
     """
     if name in ATTN_ARGS:
-        i = ATTN_ARGS[name]  # position of B; then H, Lq, Lk, D, scale, dtype
+        i = _attn_b(name, a)  # position of B; then H, Lq, Lk, D, scale, dtype
         BH, Lq, Lk, D, dt = a[i] * a[i + 1], a[i + 2], a[i + 3], a[i + 4], a[i + 6]
         mult = {"attention forward": 4.0, "attention bwd dkv": 8.0, "attention bwd dq": 2.0}[name]
         return mult * BH * Lq * Lk * D, "TFLOP/s", MFMA_BF16_PEAK if dt == 1 else MFMA_F32_PEAK, "mfma"
@@ -265,7 +271,7 @@ def kernel_work(name, a):
 
 # libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
-            "attention bwd dkv": "attn_dkv2_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
+            "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
             "chamfer_3D.forward": "chamfer_(nn|screen)_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
             "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",
             "colsum": ("colsum", "colsum_partial"),
@@ -316,7 +322,7 @@ def kernel_table(spans):
         for e0, e1, args in evs:
             key = name
             if name in ATTN_ARGS:
-                i = ATTN_ARGS[name]
+                i = _attn_b(name, args)
                 key = f"{name} [D={args[i + 4]}, {'bf16' if args[i + 6] == 1 else 'fp32'}]"
             r = rows.setdefault(key, {"name": name, "launches": 0, "ms": 0.0, "work": 0.0})
             r["launches"] += 1

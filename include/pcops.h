@@ -206,6 +206,29 @@ int pcops_attention_bwd_dkv(const void *q, const void *k, const void *v, const v
                             long long k_srow, long long v_sb, long long v_sh, long long v_srow, long long o_sb,
                             long long o_sh, long long o_srow, const void *workspace,
                             unsigned long long workspace_bytes, pcops_stream_t stream);
+/* pcops_attention_bwd_dq_delta / _dkv that also return the column sums of the
+ * gradients they store, per head over batch and rows: dq_colsum[h * D + d] =
+ * sum over (b, row) of dq(b, h, row, d) as stored (bf16), fp32 accumulation --
+ * the bias gradient of the in_proj segment that produced q (nn.MultiheadAttention's
+ * in_proj_bias, models/model_utils.py:552 / :594 self_attn / multihead_attn), so
+ * the Linear backward needs no column-sum pass over the packed gradient.  Same
+ * dk_colsum / dv_colsum for dK / dV.  bf16 only (else PCOPS_ERR_UNSUPPORTED);
+ * workspace: pcops_attention_bwd_colsum_workspace_bytes (delta first, as above,
+ * then the per-block partials), shared by the two calls in this order. */
+unsigned long long pcops_attention_bwd_colsum_workspace_bytes(int B, int H, int Lq, int Lk, int D);
+int pcops_attention_bwd_dq_delta_colsum(const void *q, const void *k, const void *v, const void *o, const void *dout,
+                                        const float *lse, void *dq, float *dq_colsum, int B, int H, int Lq, int Lk,
+                                        int D, float scale, int dtype, long long q_sb, long long q_sh,
+                                        long long q_srow, long long k_sb, long long k_sh, long long k_srow,
+                                        long long v_sb, long long v_sh, long long v_srow, long long o_sb,
+                                        long long o_sh, long long o_srow, void *workspace,
+                                        unsigned long long workspace_bytes, pcops_stream_t stream);
+int pcops_attention_bwd_dkv_colsum(const void *q, const void *k, const void *v, const void *dout, const float *lse,
+                                   void *dk, void *dv, float *dk_colsum, float *dv_colsum, int B, int H, int Lq,
+                                   int Lk, int D, float scale, int dtype, long long q_sb, long long q_sh,
+                                   long long q_srow, long long k_sb, long long k_sh, long long k_srow, long long v_sb,
+                                   long long v_sh, long long v_srow, long long o_sb, long long o_sh, long long o_srow,
+                                   void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 
 /* ---------------- attention-block glue (self_attention / cross_attention,
  * models/model_utils.py:584-617 and :542-582: the permute(2,0,1) / permute(1,2,0)

@@ -97,7 +97,7 @@ class _AttentionCore:
 
     @staticmethod
     def apply(meta, *srcs):
-        heads, scale, E, bf, qw, kw, vw = meta
+        heads, scale, E, bf, qw, kw, vw = meta[:7]   # meta[7] (bias-sum flags): GPU backward only
         q, k, v = (srcs[w[0]][..., w[1]:w[1] + E] for w in (qw, kw, vw))
         if bf:  # (B, L, E) -> (L, B, E)
             q, k, v = (t.transpose(0, 1) for t in (q, k, v))

@@ -221,13 +221,16 @@ class AttentionCore(Function):
     """o = softmax(scale q k^T) v per head.
 
     q, k and v are the column windows [off, off + E) of one to three distinct
-    source tensors (meta = (heads, scale, E, batch_first, (src, off) x 3)), so
-    packed projection outputs are read in place and their gradients written
-    in place."""
+    source tensors (meta = (heads, scale, E, batch_first, (src, off) x 3[,
+    want_sum])), so packed projection outputs are read in place and their
+    gradients written in place.  want_sum (one flag per source): the source is
+    a biased _Linear's output, so the backward (bf16) also forms each gradient's
+    column sums inside the attention passes (pcops_attention_bwd_*_colsum) and
+    hands them to that Linear's bias gradient (_attach_sum)."""
 
     @staticmethod
     def forward(ctx, meta, *srcs):
-        heads, scale, E, bf, qw, kw, vw = meta
+        heads, scale, E, bf, qw, kw, vw = meta[:7]
         srcs = tuple(s.contiguous() for s in srcs)
         for s in srcs:
             if not s.is_cuda:
@@ -250,7 +253,8 @@ class AttentionCore(Function):
                  _vptr(v_t, vw[1]), ptr(o), ptr(lse), B, heads, Lq, Lk, hd, float(scale), _DT[q_t.dtype], qb, hd, qr,
                  kb, hd, kr, vb, hd, vr, ob, hd, orow, stream_of(q_t))
         ctx.save_for_backward(*srcs, o, lse)
-        ctx.meta, ctx.dims = meta, (B, Lq, Lk, hd)
+        ctx.meta, ctx.dims = meta[:7], (B, Lq, Lk, hd)
+        ctx.want_sum = meta[7] if len(meta) > 7 else None
         return o
 
     @staticmethod
@@ -268,9 +272,28 @@ class AttentionCore(Function):
         (qb, qr), (kb, kr), (vb, vr), (ob, orow) = (_layout(t, bf) for t in (q_t, k_t, v_t, o))
         st = (qb, hd, qr, kb, hd, kr, vb, hd, vr, ob, hd, orow)
         dt = _DT[o.dtype]
+        qp, kp, vp = _vptr(q_t, qw[1]), _vptr(k_t, kw[1]), _vptr(v_t, vw[1])
+        want = ctx.want_sum
+        if (want is not None and any(want) and _ATTN_COLSUM and o.dtype == torch.bfloat16
+                and all(covered[i] == s.shape[-1] for i, s in enumerate(srcs))):
+            # one fp32 sum per source column, written by the passes in window order
+            sums = [torch.empty(s.shape[-1], dtype=torch.float32, device=o.device) for s in srcs]
+            wsb = lib().pcops_attention_bwd_colsum_workspace_bytes(B, heads, Lq, Lk, hd)
+            ws = _lib.Workspace.get(o.device, wsb)
+            with torch.cuda.device(o.device):
+                stream = stream_of(o)
+                call("attention bwd dq", lib().pcops_attention_bwd_dq_delta_colsum, qp, kp, vp, ptr(o), ptr(do),
+                     ptr(lse), _vptr(grads[qw[0]], qw[1]), _vptr(sums[qw[0]], qw[1]), B, heads, Lq, Lk, hd,
+                     float(scale), dt, *st, ptr(ws), wsb, stream)
+                call("attention bwd dkv", lib().pcops_attention_bwd_dkv_colsum, qp, kp, vp, ptr(do), ptr(lse),
+                     _vptr(grads[kw[0]], kw[1]), _vptr(grads[vw[0]], vw[1]), _vptr(sums[kw[0]], kw[1]),
+                     _vptr(sums[vw[0]], vw[1]), B, heads, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream)
+            for g, dsum, w in zip(grads, sums, want):
+                if w:
+                    _attach_sum(g, dsum)
+            return (None, *grads)
         wsb = lib().pcops_attention_bwd_workspace_bytes(B, heads, Lq, Lk, hd)
         ws = _lib.Workspace.get(o.device, wsb)
-        qp, kp, vp = _vptr(q_t, qw[1]), _vptr(k_t, kw[1]), _vptr(v_t, vw[1])
         with torch.cuda.device(o.device):
             stream = stream_of(o)
             # delta = rowsum(dO * O) is formed inside the dQ launch (bf16) and left in ws for dK/dV
@@ -357,7 +380,10 @@ class MultiheadAttention(nn.Module):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
         if dt is not None and any(s.dtype != dt for s in srcs):
             srcs = tuple(s.to(dt) for s in srcs)
-        o = AttentionCore.apply((H, scale, E, self.batch_first, *wins), *srcs)
+        # sources whose gradient feeds a _Linear bias gradient: summed inside the attention backward
+        want = tuple(self.in_proj_bias is not None and _ATTN_COLSUM and type(s.grad_fn).__name__ == "_LinearBackward"
+                     and (_FUSED_SIDE or not _lib.on_side_stream()) for s in srcs)
+        o = AttentionCore.apply((H, scale, E, self.batch_first, *wins, want), *srcs)
         return linear(o, self.out_proj.weight, self.out_proj.bias), None
 
 
@@ -627,6 +653,8 @@ _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnost
 # linear11's bias sum inside the GELU backward (A/B switch); the sum reaches the
 # Linear's backward through _attach_sum / _take_sum (stream-safe hand-off)
 _GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
+# in_proj bias sums inside the attention backward passes (A/B switch)
+_ATTN_COLSUM = os.environ.get("PCOPS_ATTN_COLSUM", "1") != "0"
 
 
 def _pos_tokens(pos):

@@ -182,6 +182,75 @@ __device__ __forceinline__ void store_Y(const f32x16 (&Y)[D / 32], T *base, long
     }
 }
 
+// Column sums of a wave's stored tile Y (D x 32 entities) over its entities, as
+// stored (bf16(Y * mul)), entities >= L counting 0: the in_proj bias gradient of
+// the projection whose output this gradient is (its column sums over all rows),
+// formed here instead of by a separate pass over the packed q/k/v gradient.
+// Reduce-scatter over the 32 entity lanes of each half: every step halves the
+// values a lane holds and pairs it with a lane differing in one more bit --
+// v_permlane16_swap (bit 4: one swap + one add per two values), then DPP
+// row_ror:8 (bit 3), row_half_mirror (bit 2, pairs l with l ^ 7), quad_perm
+// xor 2 (bit 1), each keeping the half selected by the lane's own bit, and
+// quad_perm xor 1 for the last value: 38 VALU ops per 16 values instead of a
+// 6-op wave sum for each.  Lane l ends with value j = 8 b4 + 4 b3 + 2 b2 + b1
+// (its bits), summed over its half's 32 entities; the even lanes write it.
+template <int CTRL>
+__device__ __forceinline__ float dpp_(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ float keep_send_(float lo, float hi, bool bit) {
+  const float keep = bit ? hi : lo, send = bit ? lo : hi;
+  return keep + dpp_<CTRL>(send);
+}
+template <int D>
+__device__ __forceinline__ void colsum_wave(const f32x16 (&Y)[D / 32], float mul, bool valid, float *sc, int w) {
+  const int l = lane_(), h = l >> 5;
+  const bool b3 = l & 8, b2 = l & 4, b1 = l & 2;
+  float r[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = valid ? (float)(__bf16)(Y[db][j] * mul) : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // bit 4: rows 0/2 keep v[j], rows 1/3 keep v[j + 8]
+      const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 8]), false, false);
+      v[j] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = keep_send_<0x128>(v[j], v[j + 4], b3);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) v[j] = keep_send_<0x141>(v[j], v[j + 2], b2);
+    v[0] = keep_send_<0x4E>(v[0], v[1], b1);
+    r[db] = v[0] + dpp_<0xB1>(v[0]);
+  }
+  if ((l & 1) == 0) {
+    const int j = ((l >> 4) & 1) * 8 + (b3 ? 4 : 0) + (b2 ? 2 : 0) + (b1 ? 1 : 0);
+    const int d0 = 8 * (j >> 2) + 4 * h + (j & 3);
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) sc[w * D + db * 32 + d0] = r[db];
+  }
+}
+
+// the partial row of block (bh, rb): row b * nrb + rb, columns h * D .. h * D + D - 1 of a
+// (B * nrb, H * D) array, so the final sum is a plain column sum over its rows
+__device__ __forceinline__ long long colsum_row(int bh, int rb, int H, int D) {
+  const int b = bh / H, h = bh - b * H;
+  return ((long long)(b * (int)gridDim.x + rb) * H + h) * D;
+}
+
+// after colsum_wave in every wave and a barrier: part_row[d] = sum over the NW waves in order
+template <int D, int NW>
+__device__ __forceinline__ void colsum_block(const float *sc, float *part_row) {
+  for (int d = threadIdx.x; d < D; d += NW * 64) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += sc[w * D + d];
+    part_row[d] = t;
+  }
+}
+
 // Element (b, h, row, d) of a tensor lives at b*sb + h*sh + row*srow + d, so
 // seq-first (L, B, H*hd) [sb = H*hd, sh = hd, srow = B*H*hd] and batch-first
 // (B, L, H*hd) [sb = L*H*hd, sh = hd, srow = H*hd] layouts are both read in place.
@@ -736,13 +805,14 @@ int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse
 // hold the two halves of the row: one permlane32 swap adds them) and written
 // to delta_out for the dK/dV pass -- no separate preprocess launch, no second
 // read of dO.
-template <int D, int NW, int OCC, bool FD, bool HS>
+template <int D, int NW, int OCC, bool FD, bool HS, bool CS>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dq2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
                                                            const __bf16 *__restrict__ V, const __bf16 *__restrict__ dO,
                                                            const float *__restrict__ lse,
                                                            const float *__restrict__ delta, __bf16 *__restrict__ dQ,
                                                            int Lq, int Lk, float scale, Strides st,
-                                                           const __bf16 *__restrict__ O, float *__restrict__ delta_out) {
+                                                           const __bf16 *__restrict__ O, float *__restrict__ delta_out,
+                                                           float *__restrict__ cpart) {
   using C = Fwd2Cfg<D, NW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char bwd2_smem[];
   __bf16 *sk = reinterpret_cast<__bf16 *>(bwd2_smem);
@@ -842,6 +912,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
   for (int t = 0; t < nfull; ++t) tile(t, std::false_type{});
   if (nfull < ntiles) tile(nfull, std::true_type{});
   store_Y<__bf16, D>(Y, dQ + st.q_off(bh), st.q_srow, q0, Lq, scale);
+  if constexpr (CS) {  // the tiles' LDS is free: the last tile ended with a barrier
+    float *sc = reinterpret_cast<float *>(bwd2_smem);
+    colsum_wave<D>(Y, scale, qi < Lq, sc, w);
+    lds_barrier();
+    colsum_block<D, NW>(sc, cpart + colsum_row(bh, rb, st.H, D));
+  }
 }
 
 // dK/dV pass: keys on the lane, Q/dO 64-row tiles (+ their lse/delta) double-buffered.
@@ -849,7 +925,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
 // live).  MODE 1: dV only, MODE 2: dK only -- half the accumulators, so OCC = 2
 // waves per SIMD fit; the split pays one extra S recompute (5 instead of 4
 // GEMM units per key) for the second wave's latency hiding.
-template <int D, int NW, int MODE, int OCC>
+template <int D, int NW, int MODE, int OCC, bool CS>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dkv2_kernel(const __bf16 *__restrict__ Q,
                                                             const __bf16 *__restrict__ K,
                                                             const __bf16 *__restrict__ V,
@@ -857,7 +933,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
                                                             const float *__restrict__ lse,
                                                             const float *__restrict__ delta, __bf16 *__restrict__ dK,
                                                             __bf16 *__restrict__ dV, int Lq, int Lk, float scale,
-                                                            Strides st) {
+                                                            Strides st, float *__restrict__ cpart_k,
+                                                            float *__restrict__ cpart_v) {
   using C = Fwd2Cfg<D, NW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char bwd2_smem[];
   __bf16 *sq = reinterpret_cast<__bf16 *>(bwd2_smem);
@@ -970,6 +1047,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
   }
   if (MODE != 2) store_Y<__bf16, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
   if (MODE != 1) store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
+  if constexpr (CS) {  // the tiles' LDS is free: the last tile ended with a barrier
+    float *sc = reinterpret_cast<float *>(bwd2_smem);
+    const long long row = colsum_row(bh, rb, st.H, D);
+    if (MODE != 2) colsum_wave<D>(Y1, 1.f, ki < Lk, sc, w);
+    if (MODE != 1) colsum_wave<D>(Y2, scale, ki < Lk, sc + NW * D, w);
+    lds_barrier();
+    if (MODE != 2) colsum_block<D, NW>(sc, cpart_v + row);
+    if (MODE != 1) colsum_block<D, NW>(sc + NW * D, cpart_k + row);
+  }
 }
 
 // ----------------------------------------------------------------- dK/dV, one pass, software-pipelined (v3)
@@ -1147,11 +1233,12 @@ __device__ __forceinline__ void dkv3_c(f32x16 (&Y1)[D / 32], f32x16 (&Y2)[D / 32
     }
 }
 
-template <int D, int OCC>
+template <int D, int OCC, bool CS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dkv3_kernel(
     const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K, const __bf16 *__restrict__ V,
     const __bf16 *__restrict__ dO, const float *__restrict__ lse, const float *__restrict__ delta,
-    __bf16 *__restrict__ dK, __bf16 *__restrict__ dV, int Lq, int Lk, float scale, Strides st) {
+    __bf16 *__restrict__ dK, __bf16 *__restrict__ dV, int Lq, int Lk, float scale, Strides st,
+    float *__restrict__ cpart_k, float *__restrict__ cpart_v) {
   constexpr int NW = 4, RS = Img<D>::RS, TB = kKT * RS;  // TB: elements per tile slot
   constexpr int kCPT = kKT * D / 8 / (NW * 64);           // 16-B chunks per thread per tile
   static_assert(kKT * D / 8 % (NW * 64) == 0, "tile chunks must split evenly");
@@ -1292,6 +1379,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   }
   store_Y<__bf16, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
   store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
+  if constexpr (CS) {
+    lds_barrier();  // every wave is past its last ring read
+    float *sc = reinterpret_cast<float *>(dkv3_smem);
+    const long long row = colsum_row(bh, rb, st.H, D);
+    colsum_wave<D>(Y1, 1.f, kv, sc, w);
+    colsum_wave<D>(Y2, scale, kv, sc + NW * D, w);
+    lds_barrier();
+    colsum_block<D, NW>(sc, cpart_v + row);
+    colsum_block<D, NW>(sc + NW * D, cpart_k + row);
+  }
 }
 
 // D = 64 runs 4-wave blocks at 3 waves per SIMD (the key-half split fits
@@ -1303,20 +1400,29 @@ struct Dq2Cfg {
   static constexpr int kOcc = kHS ? (D == 64 ? 3 : 2) : (D <= 96 || NW == 8) ? 2 : 1;
 };
 
-template <int D, int NW, bool FD>
+// per-block column partial sums of the gradients a backward launch stores (the
+// *_colsum entry points): dQ in `a`; dK in `a`, dV in `b`; row (bh * nrb + rb) of
+// D floats each, nrb = the launch's row blocks per (batch, head), set by the launcher
+struct ColPart {
+  float *a = nullptr, *b = nullptr;
+  int nrb = 0;
+};
+
+template <int D, int NW, bool FD, bool CS>
 int launch_dq2_impl(const void *q, const void *k, const void *v, const void *dout, const float *lse,
                     const float *delta, void *dq, int BH, int Lq, int Lk, float scale, const Strides &st,
-                    const void *o, float *delta_out, hipStream_t s) {
+                    const void *o, float *delta_out, hipStream_t s, ColPart *cp) {
   using C = Fwd2Cfg<D, NW>;
   constexpr int OCC = Dq2Cfg<D, NW>::kOcc;
   constexpr bool HS = Dq2Cfg<D, NW>::kHS;
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC, FD, HS>,
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC, FD, HS, CS>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD, HS>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+  if (cp) cp->nrb = grid.x;
+  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD, HS, CS>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
                      (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dq, Lq, Lk,
-                     scale, st, (const __bf16 *)o, delta_out);
+                     scale, st, (const __bf16 *)o, delta_out, cp ? cp->a : nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
@@ -1325,9 +1431,11 @@ int launch_dq2_impl(const void *q, const void *k, const void *v, const void *dou
 template <int D, int NW>
 int launch_dq2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                void *dq, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s,
-               const void *o = nullptr, float *delta_out = nullptr) {
-  return o ? launch_dq2_impl<D, NW, true>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, o, delta_out, s)
-           : launch_dq2_impl<D, NW, false>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, o, delta_out, s);
+               const void *o = nullptr, float *delta_out = nullptr, ColPart *cp = nullptr) {
+  if (cp) return o ? launch_dq2_impl<D, NW, true, true>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, o, delta_out, s, cp)
+                  : PCOPS_ERR_UNSUPPORTED;  // the column sums ride on the fused-delta pass
+  return o ? launch_dq2_impl<D, NW, true, false>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, o, delta_out, s, cp)
+           : launch_dq2_impl<D, NW, false, false>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, o, delta_out, s, cp);
 }
 
 bool dkv_split() {  // PCOPS_DKV_SPLIT=0 keeps the one-pass dK/dV kernel for D = 128 (A/B runs)
@@ -1340,35 +1448,38 @@ bool dkv_split() {  // PCOPS_DKV_SPLIT=0 keeps the one-pass dK/dV kernel for D =
 
 // one dK/dV launch of a given shape: NW waves per block, MODE (0 one pass, 3 one pass by
 // 32-query halves -- the same per-accumulator order as 0, half the live S / dP), OCC waves / SIMD
-template <int D, int NW, int MODE, int OCC>
+template <int D, int NW, int MODE, int OCC, bool CS>
 int launch_dkv2_cfg(const void *q, const void *k, const void *v, const void *dout, const float *lse,
                     const float *delta, void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st,
-                    hipStream_t s) {
+                    hipStream_t s, ColPart *cp) {
   using C = Fwd2Cfg<D, NW>;
   const size_t lds = C::kLds + 4 * kKT * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW, MODE, OCC>,
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW, MODE, OCC, CS>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, MODE, OCC>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
+  if (cp) cp->nrb = grid.x;
+  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, MODE, OCC, CS>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
                      (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
-                     (__bf16 *)dv, Lq, Lk, scale, st);
+                     (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
 
-template <int D, int OCC>
+template <int D, int OCC, bool CS>
 int launch_dkv3(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
-                void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
+                void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s,
+                ColPart *cp) {
   if ((long long)kKT * (st.q_srow > st.o_srow ? st.q_srow : st.o_srow) >= (1ll << 31)) return PCOPS_ERR_UNSUPPORTED;
   const size_t lds = 6ull * kKT * Img<D>::RS * sizeof(__bf16) + 6 * kKT * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv3_kernel<D, OCC>,
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv3_kernel<D, OCC, CS>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lk + 127) / 128, BH);
-  hipLaunchKernelGGL((attn_dkv3_kernel<D, OCC>), grid, dim3(256), lds, s, (const __bf16 *)q, (const __bf16 *)k,
+  if (cp) cp->nrb = grid.x;
+  hipLaunchKernelGGL((attn_dkv3_kernel<D, OCC, CS>), grid, dim3(256), lds, s, (const __bf16 *)q, (const __bf16 *)k,
                      (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk, (__bf16 *)dv, Lq, Lk, scale,
-                     st);
+                     st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
@@ -1382,84 +1493,95 @@ int dkv3_mode() {
   return v;
 }
 
-template <int D, int NW>
-int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
-                void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s) {
+template <int D, int NW, bool CS>
+int launch_dkv2_cs(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+                void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s,
+                ColPart *cp = nullptr) {
   using C = Fwd2Cfg<D, NW>;
   if constexpr (D >= 64) {
     const int m3 = dkv3_mode();
     if (m3 == 1 || (m3 < 0 && D >= 96)) {
-      const int rc = launch_dkv3<D, 1>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      const int rc = launch_dkv3<D, 1, CS>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
       if (rc != PCOPS_ERR_UNSUPPORTED) return rc;  // strides too large for its 32-bit tile offsets: v2 below
     }
   }
-  if constexpr (D == 64 && NW == 8) {
+  if constexpr (D == 64 && NW == 8 && !CS) {
     // occupancy variants of the long-sequence D = 64 pass (A/B: PCOPS_DKV64)
     static const int var = env_int("PCOPS_DKV64", 0);
     switch (var) {
-      case 1: return launch_dkv2_cfg<64, 4, 3, 2>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
-      case 2: return launch_dkv2_cfg<64, 4, 3, 3>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
-      case 3: return launch_dkv2_cfg<64, 8, 3, 2>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
-      case 4: return launch_dkv2_cfg<64, 4, 0, 2>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      case 1: return launch_dkv2_cfg<64, 4, 3, 2, CS>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
+      case 2: return launch_dkv2_cfg<64, 4, 3, 3, CS>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
+      case 3: return launch_dkv2_cfg<64, 8, 3, 2, CS>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
+      case 4: return launch_dkv2_cfg<64, 4, 0, 2, CS>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
       default: break;
     }
   }
   const size_t lds = C::kLds + 4 * kKT * sizeof(float);
   const dim3 grid((Lk + NW * 32 - 1) / (NW * 32), BH);
-  if constexpr (D == 128) {
+  if constexpr (D == 128 && !CS) {
     // one-pass variants of the D = 128 dK/dV (A/B: PCOPS_DKV128): by 32-query halves, 1 wave per SIMD
     static const int var = env_int("PCOPS_DKV128", 0);
-    if (var == 1) return launch_dkv2_cfg<128, 4, 3, 1>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+    if (var == 1) return launch_dkv2_cfg<128, 4, 3, 1, CS>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
   }
   if (D >= 96 && dkv_split()) {
     // 8 waves per block halve each thread's share of the tile prefetch
     using C8 = Fwd2Cfg<D, 8>;
     const size_t lds8 = C8::kLds + 4 * kKT * sizeof(float);
     const dim3 grid8((Lk + 8 * 32 - 1) / (8 * 32), BH);
-    static const hipError_t a1 = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, 8, 1, 2>,
+    if (cp) cp->nrb = grid8.x;
+    static const hipError_t a1 = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, 8, 1, 2, CS>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
-    static const hipError_t a2 = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, 8, 2, 2>,
+    static const hipError_t a2 = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, 8, 2, 2, CS>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
     if (a1 != hipSuccess || a2 != hipSuccess) return PCOPS_ERR_LAUNCH;
-    hipLaunchKernelGGL((attn_dkv2_kernel<D, 8, 1, 2>), grid8, dim3(C8::kThr), lds8, s, (const __bf16 *)q,
+    hipLaunchKernelGGL((attn_dkv2_kernel<D, 8, 1, 2, CS>), grid8, dim3(C8::kThr), lds8, s, (const __bf16 *)q,
                        (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
-                       (__bf16 *)dv, Lq, Lk, scale, st);
+                       (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
     PC_CHECK_LAUNCH();
-    hipLaunchKernelGGL((attn_dkv2_kernel<D, 8, 2, 2>), grid8, dim3(C8::kThr), lds8, s, (const __bf16 *)q,
+    hipLaunchKernelGGL((attn_dkv2_kernel<D, 8, 2, 2, CS>), grid8, dim3(C8::kThr), lds8, s, (const __bf16 *)q,
                        (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
-                       (__bf16 *)dv, Lq, Lk, scale, st);
+                       (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
     PC_CHECK_LAUNCH();
     return PCOPS_OK;
   }
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW, 0, 1>,
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW, 0, 1, CS>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
-  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, 0, 1>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
+  if (cp) cp->nrb = grid.x;
+  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, 0, 1, CS>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
                      (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
-                     (__bf16 *)dv, Lq, Lk, scale, st);
+                     (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
 
+template <int D, int NW>
+int launch_dkv2(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
+                void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s,
+                ColPart *cp = nullptr) {
+  return cp ? launch_dkv2_cs<D, NW, true>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp)
+            : launch_dkv2_cs<D, NW, false>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
+}
+
 int dq2_dispatch(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                  void *dq, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s,
-                 const void *o = nullptr, float *delta_out = nullptr) {
+                 const void *o = nullptr, float *delta_out = nullptr, ColPart *cp = nullptr) {
   const bool wide = Lq > 128;
   switch (D) {
     case 32:
-      return wide ? launch_dq2<32, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
-                  : launch_dq2<32, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+      return wide ? launch_dq2<32, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out, cp)
+                  : launch_dq2<32, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out, cp);
     case 64: {
       static const int nw4 = env_int("PCOPS_DQ_NW4", 1);
-      return (wide && !nw4) ? launch_dq2<64, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
-                            : launch_dq2<64, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+      return (wide && !nw4) ? launch_dq2<64, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out, cp)
+                            : launch_dq2<64, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out, cp);
     }
     case 96:
-      return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+      return launch_dq2<96, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out, cp);
     case 128: {
       static const int nw4 = env_int("PCOPS_DQ128_NW4", 0);   // A/B: 4-wave key-half blocks at any length
-      return (wide && !nw4) ? launch_dq2<128, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out)
-                            : launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out);
+      return (wide && !nw4) ? launch_dq2<128, 8>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out, cp)
+                            : launch_dq2<128, 4>(q, k, v, dout, lse, delta, dq, BH, Lq, Lk, scale, st, s, o, delta_out, cp);
     }
     default:
       return PCOPS_ERR_UNSUPPORTED;
@@ -1467,19 +1589,20 @@ int dq2_dispatch(const void *q, const void *k, const void *v, const void *dout, 
 }
 
 int dkv2_dispatch(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
-                  void *dk, void *dv, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s) {
+                  void *dk, void *dv, int BH, int Lq, int Lk, int D, float scale, const Strides &st, hipStream_t s,
+                  ColPart *cp = nullptr) {
   const bool wide = Lk > 128;
   switch (D) {
     case 32:
-      return wide ? launch_dkv2<32, 8>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s)
-                  : launch_dkv2<32, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      return wide ? launch_dkv2<32, 8>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp)
+                  : launch_dkv2<32, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
     case 64:
-      return wide ? launch_dkv2<64, 8>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s)
-                  : launch_dkv2<64, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      return wide ? launch_dkv2<64, 8>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp)
+                  : launch_dkv2<64, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
     case 96:
-      return launch_dkv2<96, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      return launch_dkv2<96, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
     case 128:
-      return launch_dkv2<128, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s);
+      return launch_dkv2<128, 4>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cp);
     default:
       return PCOPS_ERR_UNSUPPORTED;
   }
@@ -1593,6 +1716,41 @@ int launch_dkv(const void *q, const void *k, const void *v, const void *dout, co
 #undef ATT_DKV
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
+}
+
+// out_s[c] = sum over r < n of part_s[r * C + c] for one or two (part, out) segments
+// (the per-block partial rows of dQ, or of dK and dV, C = H * D): 32 columns x 32 row
+// groups per block, each group in row order, then the groups in order -- a fixed
+// order for a given launch shape.  Blocks [0, C / 32) sum segment 0, the rest segment 1.
+__global__ __launch_bounds__(1024) void attn_colsum_reduce_kernel(const float *__restrict__ p0, float *__restrict__ o0,
+                                                                  const float *__restrict__ p1, float *__restrict__ o1,
+                                                                  int n, int C) {
+  __shared__ float red[32][33];
+  const int nb = C / 32, seg = (int)blockIdx.x >= nb;
+  const float *part = seg ? p1 : p0;
+  float *out = seg ? o1 : o0;
+  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5, col = ((int)blockIdx.x - seg * nb) * 32 + cl;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int r = grp; r < n; r += 32) acc += part[(long long)r * C + col];
+  red[grp][cl] = acc;
+  __syncthreads();
+  if (grp == 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) sum += red[i][cl];
+    out[col] = sum;
+  }
+}
+
+int launch_colsum_reduce(const float *p0, float *o0, const float *p1, float *o1, int n, int C, hipStream_t s) {
+  hipLaunchKernelGGL(attn_colsum_reduce_kernel, dim3((p1 ? 2 : 1) * C / 32), dim3(1024), 0, s, p0, o0, p1, o1, n, C);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+unsigned long long delta_bytes(int B, int H, int Lq) {
+  return ((unsigned long long)B * H * Lq * sizeof(float) + 255) & ~255ull;
 }
 
 int check_common(int BH, int Lq, int Lk, int D, int dtype) {
@@ -1723,6 +1881,80 @@ extern "C" int pcops_attention_bwd_dkv(const void *q, const void *k, const void 
   if (dtype == 0) return launch_dkv<float>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
   if (use_v1()) return launch_dkv<__bf16>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
   return dkv2_dispatch(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, D, scale, st, s);
+}
+
+// The same two passes, each also forming the column sums of the gradients it
+// stores (per head, over batch and rows: out[h * D + d]) -- the bias gradient of
+// the projection that produced q / k / v, without a pass over the gradient.
+extern "C" unsigned long long pcops_attention_bwd_colsum_workspace_bytes(int B, int H, int Lq, int Lk, int D) {
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || D <= 0) return 0;
+  const long long rq = (Lq + 127) / 128, rk = 2 * ((Lk + 127) / 128);
+  return delta_bytes(B, H, Lq) + (unsigned long long)B * H * (rq > rk ? rq : rk) * D * sizeof(float);
+}
+
+extern "C" int pcops_attention_bwd_dq_delta_colsum(const void *q, const void *k, const void *v, const void *o,
+                                                   const void *dout, const float *lse, void *dq, float *dq_colsum,
+                                                   int B, int H, int Lq, int Lk, int D, float scale, int dtype,
+                                                   PC_ATTN_STRIDES, void *workspace, unsigned long long workspace_bytes,
+                                                   pcops_stream_t stream) {
+  if (B < 0 || H <= 0) return PCOPS_ERR_INVALID;
+  int rc = check_common(B * H, Lq, Lk, D, dtype);
+  if (rc) return rc;
+  if (dtype != 1 || use_v1()) return PCOPS_ERR_UNSUPPORTED;  // the bf16 MFMA passes only
+  const int BH = B * H;
+  if (!dq_colsum) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (BH == 0) return PCOPS_OK;
+  if (Lq == 0) return hipMemsetAsync(dq_colsum, 0, (size_t)H * D * sizeof(float), s) == hipSuccess ? PCOPS_OK
+                                                                                              : PCOPS_ERR_LAUNCH;
+  if (!q || !k || !v || !o || !dout || !lse || !dq || Lk <= 0) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_colsum_workspace_bytes(B, H, Lq, Lk, D))
+    return PCOPS_ERR_WORKSPACE;
+  if (!aligned_ok(q, q_sb, q_sh, q_srow, 2) || !aligned_ok(k, k_sb, k_sh, k_srow, 2) ||
+      !aligned_ok(v, v_sb, v_sh, v_srow, 2) || !aligned_ok(dout, o_sb, o_sh, o_srow, 2) ||
+      !aligned_ok(o, o_sb, o_sh, o_srow, 2) || !aligned_ok(dq, q_sb, q_sh, q_srow, 2))
+    return PCOPS_ERR_UNSUPPORTED;
+  const Strides st{PC_ATTN_STRIDE_ARGS, H};
+  ColPart cp;
+  cp.a = (float *)((char *)workspace + delta_bytes(B, H, Lq));
+  rc = dq2_dispatch(q, k, v, dout, lse, nullptr, dq, BH, Lq, Lk, D, scale, st, s, o, (float *)workspace, &cp);
+  if (rc) return rc;
+  return launch_colsum_reduce(cp.a, dq_colsum, nullptr, nullptr, B * cp.nrb, H * D, s);
+}
+
+extern "C" int pcops_attention_bwd_dkv_colsum(const void *q, const void *k, const void *v, const void *dout,
+                                              const float *lse, void *dk, void *dv, float *dk_colsum, float *dv_colsum,
+                                              int B, int H, int Lq, int Lk, int D, float scale, int dtype,
+                                              PC_ATTN_STRIDES, void *workspace, unsigned long long workspace_bytes,
+                                              pcops_stream_t stream) {
+  if (B < 0 || H <= 0) return PCOPS_ERR_INVALID;
+  int rc = check_common(B * H, Lq, Lk, D, dtype);
+  if (rc) return rc;
+  if (dtype != 1 || use_v1()) return PCOPS_ERR_UNSUPPORTED;
+  const int BH = B * H;
+  if (!dk_colsum || !dv_colsum) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (BH == 0) return PCOPS_OK;
+  if (Lk == 0) {
+    if (hipMemsetAsync(dk_colsum, 0, (size_t)H * D * sizeof(float), s) != hipSuccess ||
+        hipMemsetAsync(dv_colsum, 0, (size_t)H * D * sizeof(float), s) != hipSuccess)
+      return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!q || !k || !v || !dout || !lse || !dk || !dv || Lq <= 0) return PCOPS_ERR_INVALID;
+  if (!workspace || workspace_bytes < pcops_attention_bwd_colsum_workspace_bytes(B, H, Lq, Lk, D))
+    return PCOPS_ERR_WORKSPACE;
+  if (!aligned_ok(q, q_sb, q_sh, q_srow, 2) || !aligned_ok(k, k_sb, k_sh, k_srow, 2) ||
+      !aligned_ok(v, v_sb, v_sh, v_srow, 2) || !aligned_ok(dout, o_sb, o_sh, o_srow, 2) ||
+      !aligned_ok(dk, k_sb, k_sh, k_srow, 2) || !aligned_ok(dv, v_sb, v_sh, v_srow, 2))
+    return PCOPS_ERR_UNSUPPORTED;
+  const Strides st{PC_ATTN_STRIDE_ARGS, H};
+  ColPart cp;
+  cp.a = (float *)((char *)workspace + delta_bytes(B, H, Lq));
+  cp.b = cp.a + (long long)BH * ((Lk + 127) / 128) * D;
+  rc = dkv2_dispatch(q, k, v, dout, lse, (const float *)workspace, dk, dv, BH, Lq, Lk, D, scale, st, s, &cp);
+  if (rc) return rc;
+  return launch_colsum_reduce(cp.a, dk_colsum, cp.b, dv_colsum, B * cp.nrb, H * D, s);
 }
 
 // dq/dk/dv use the q/k/v strides; dout uses the o strides.

@@ -782,3 +782,57 @@ def test_gelu_backward_kernel(dev, dt, rows, C):
     assert A._take_sum(du) is None   # handed over exactly once
     torch.testing.assert_close(dsum, du.float().sum(0), rtol=1e-4, atol=1e-3)
 
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,E,packed,bf", [
+    (2, 8, 2048, 2048, 512, True, False),    # refine2 self-attention (hd 64), one (L, B, 3E) source
+    (2, 8, 2048, 2048, 1024, True, True),    # hd 128, batch-first
+    (1, 8, 333, 250, 1024, False, False),    # ragged cross, hd 128 (the pipelined dK/dV pass)
+    (1, 8, 512, 512, 768, True, True),       # hd 96
+    (2, 2, 70, 130, 64, False, True),        # hd 32, ragged
+    (3, 4, 49, 49, 512, True, False),        # short rows: one partial block per (batch, head)
+    (2, 4, 130, 129, 128, False, False)])
+def test_attention_bwd_colsum(dev, B, H, Lq, Lk, E, packed, bf):
+    """pcops_attention_bwd_*_colsum: the gradients are bitwise those of the plain
+    passes, and the column sums they hand to the in_proj bias gradient equal the
+    float64 column sums of the stored bf16 gradients (fp32 accumulation bound)."""
+    from svdformer_pointsea_amd.attention import AttentionCore, _take_sum
+
+    got = {}
+
+    class Grab(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, i):
+            ctx.i = i
+            return x.clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            got[ctx.i] = (g.clone(), _take_sum(g))
+            return g, None
+
+    gen = torch.Generator().manual_seed(11)
+    shp = (lambda L, W: (B, L, W)) if bf else (lambda L, W: (L, B, W))
+    if packed:
+        assert Lq == Lk
+        srcs = [torch.randn(*shp(Lq, 3 * E), generator=gen)]
+        wins = ((0, 0), (0, E), (0, 2 * E))
+    else:
+        srcs = [torch.randn(*shp(Lq, E), generator=gen), torch.randn(*shp(Lk, 2 * E), generator=gen)]
+        wins = ((0, 0), (1, 0), (1, E))
+    srcs = [s.to(dev, torch.bfloat16).requires_grad_(True) for s in srcs]
+    g = torch.randn(*shp(Lq, E), generator=gen).to(dev, torch.bfloat16)
+    scale = 1.0 / math.sqrt(E // H)
+    res = []
+    for want in (None, (True,) * len(srcs)):
+        got.clear()
+        meta = (H, scale, E, bf, *wins) + ((want,) if want else ())
+        o = AttentionCore.apply(meta, *[Grab.apply(s, i) for i, s in enumerate(srcs)])
+        o.backward(g)
+        res.append([got[i] for i in range(len(srcs))])
+    for (g0, s0), (g1, s1) in zip(*res):
+        assert s0 is None and s1 is not None and s1.dtype == torch.float32
+        assert torch.equal(g0, g1)
+        ref = g1.double().reshape(-1, g1.shape[-1]).sum(0)
+        bound = 2e-6 * g1.double().abs().reshape(-1, g1.shape[-1]).sum(0) + 1e-6
+        assert ((s1.double() - ref).abs() <= bound).all(), (s1.double() - ref).abs().max().item()
