@@ -407,6 +407,7 @@ void add_go(const void *a, const void *b, void *out, long long n8, hipStream_t s
 // stored once.  Stage 2: 32 columns x 32 chunk groups per block add the
 // <= 1024 partial rows in a fixed order (deterministic, no atomics).
 constexpr int kCsMaxChunks = 1024;
+constexpr int kCsU = 8;
 
 template <int DT>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restrict__ g, long long rows, int C, int V,
@@ -420,14 +421,23 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restr
   float acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  // kCsU rows per lane per batch, their loads issued together (rows past r1 read a
+  // valid row and count 0): a runtime-count `#pragma unroll` loop here compiled to
+  // one load + vmcnt(0) per row (2.5 TB/s)
   const long long step = 4LL * rw;
-  long long r = r0 + w * rw + rsub;
-#pragma unroll 16
-  for (; r < r1; r += step) {
-    V8 t;
-    ld8c<DT>(t, g, r * C + col);
+  for (long long rb = r0 + w * rw + rsub; rb < r1; rb += kCsU * step) {
+    V8 t[kCsU];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] += t.v[k];
+    for (int u = 0; u < kCsU; ++u) {
+      const long long r = rb + u * step;
+      ld8c<DT>(t[u], g, (r < r1 ? r : rb) * C + col);
+    }
+#pragma unroll
+    for (int u = 0; u < kCsU; ++u) {
+      const bool ok = rb + u * step < r1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += ok ? t[u].v[k] : 0.f;
+    }
   }
   for (int o = V; o < 64; o <<= 1)
 #pragma unroll
@@ -492,27 +502,38 @@ __global__ __launch_bounds__(256) void gelu_bwd_partial_kernel(const void *__res
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
   const long long step = 4LL * rw;
-#pragma unroll 4
-  for (long long r = r0 + w * rw + rsub; r < r1; r += step) {
-    V8 g, x, o;
-    ld8c<DT>(g, dy, r * C + col);
-    ld8c<DT>(x, u, r * C + col);
+  constexpr int U = 4;  // rows per lane per batch, loads issued together (see colsum_partial_kernel)
+  for (long long rb = r0 + w * rw + rsub; rb < r1; rb += U * step) {
+    V8 g[U], x[U];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float cdf = 0.5f * (1.0f + erff(x.v[k] * kAlpha));
-      const float pdf = expf(-0.5f * x.v[k] * x.v[k]) * kBeta;
-      o.v[k] = g.v[k] * (cdf + x.v[k] * pdf);
+    for (int i = 0; i < U; ++i) {
+      const long long r = rb + i * step;
+      const long long e = (r < r1 ? r : rb) * C + col;
+      ld8c<DT>(g[i], dy, e);
+      ld8c<DT>(x[i], u, e);
     }
-    if constexpr (DT == 0) {
-      st8_f32(reinterpret_cast<float *>(du), r * C + col, o);
-    } else {
-      st8_bf16(reinterpret_cast<__bf16 *>(du), r * C + col, o);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o.v[k] = (float)(__bf16)o.v[k];  // the sum sees du as stored
+    for (int i = 0; i < U; ++i) {
+      const long long r = rb + i * step;
+      const bool ok = r < r1;
+      V8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float cdf = 0.5f * (1.0f + erff(x[i].v[k] * kAlpha));
+        const float pdf = expf(-0.5f * x[i].v[k] * x[i].v[k]) * kBeta;
+        o.v[k] = g[i].v[k] * (cdf + x[i].v[k] * pdf);
+      }
+      if constexpr (DT == 0) {
+        if (ok) st8_f32(reinterpret_cast<float *>(du), r * C + col, o);
+      } else {
+        if (ok) st8_bf16(reinterpret_cast<__bf16 *>(du), r * C + col, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = (float)(__bf16)o.v[k];  // the sum sees du as stored
+      }
+      if constexpr (SUM)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += ok ? o.v[k] : 0.f;
     }
-    if constexpr (SUM)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += o.v[k];
   }
   if constexpr (SUM) {
     for (int o = V; o < 64; o <<= 1)
