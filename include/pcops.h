@@ -294,6 +294,11 @@ int pcops_wgrad_skinny(const void *g, const void *x, long long T, int Co, int Ci
 unsigned long long pcops_colsum_workspace_bytes(long long rows, int C);
 int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype, void *workspace,
                  unsigned long long workspace_bytes, pcops_stream_t stream);
+/* pcops_colsum_ld: the same over rows ld elements apart (ld >= C, ld % 8 == 0): a channel slice of a
+ *   wider gradient (the Linear's output was concatenated / split after it) summed in place instead of
+ *   after a contiguous copy. */
+int pcops_colsum_ld(const void *g, int g_dtype, long long rows, int C, long long ld, void *out, int out_dtype,
+                    void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 
 /* ---------------- BatchNorm (+ residual) (+ ReLU / LeakyReLU) on channels_last activations ----------------
  * Replaces torch.nn.BatchNorm2d's forward / backward (MIOpen) together with the activation and

@@ -71,6 +71,7 @@ _SIGS = {
     "pcops_wgrad_skinny": (I, [P, P, LL, I, I, P, I, P, ULL, P]),
     "pcops_colsum_workspace_bytes": (ULL, [LL, I]),
     "pcops_colsum": (I, [P, I, LL, I, P, I, P, ULL, P]),
+    "pcops_colsum_ld": (I, [P, I, LL, I, LL, P, I, P, ULL, P]),
     "pcops_batchnorm_workspace_bytes": (ULL, [LL, I]),
     "pcops_batchnorm_fwd": (I, [P, I, P, I, LL, I, P, P, P, P, F, F, I, I, F, P, P, P, P, ULL, P, P]),
     "pcops_batchnorm_bwd": (I, [P, P, P, I, LL, I, P, P, P, I, I, F, P, P, P, P, P, ULL, P]),

@@ -57,6 +57,8 @@ def _wgrad(g2, x2, wdt):
     weight dtype -- 2-4x faster at these shapes (tools/gemm_bench.py)."""
     T, Cout = g2.shape
     Cin = x2.shape[1]
+    if Cin == 6 and not g2.is_contiguous():
+        g2 = g2.contiguous()
     if (Cin == 6 and Cout % 8 == 0 and Cout <= 64 and g2.is_cuda and g2.dtype == torch.bfloat16
             and x2.dtype == torch.bfloat16 and wdt in _DT and g2.data_ptr() % 16 == 0):
         # EdgeConv's 6 -> Cout conv: one streaming pass (as a split-K bmm it ran at 1.5 TFLOP/s)
@@ -100,6 +102,9 @@ class _Linear(Function):
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
     def forward(ctx, x, w, b, b_dtype=None):
         ctx.save_for_backward(x, w)
+        if _DEBUG_CONTIG:   # diagnostic: where the backward's operand copies come from
+            import traceback
+            ctx.site = " < ".join(f"{f.name}:{f.lineno}" for f in traceback.extract_stack(limit=7)[-7:-1][::-1])
         ctx.has_b = b is not None
         ctx.b_dtype = b_dtype   # the bias's own dtype (custom_fwd hands forward the bf16 cast)
         # on a side stream: GEMMs without stream-K (forward here, backward on
@@ -112,19 +117,27 @@ class _Linear(Function):
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, g):
         x, w = ctx.saved_tensors
+        if _DEBUG_CONTIG and (not g.is_contiguous() or not x.is_contiguous()):
+            import sys
+            print(f"[contig] g {tuple(g.shape)} {g.stride()} x {tuple(x.shape)} {x.stride()} at {ctx.site}",
+                  file=sys.stderr)
         C = g.shape[-1]
         g2 = g.reshape(-1, C)
+        if not g2.is_contiguous() and not (_STRIDED_G and _row_strided(g2)):
+            g2 = g2.contiguous()   # once, for all three uses
+        # else g is a channel slice of a wider gradient (the output was concatenated with
+        # others): the GEMMs read it with a leading dimension, colsum with a row stride
         gx = gw = gb = None
         with _lib.no_stream_k() if ctx.side else _nullctx():
             if ctx.needs_input_grad[0]:
                 gx = (g2 @ w).view(x.shape)
             if ctx.needs_input_grad[1]:
-                gw = _wgrad(g2.contiguous(), x.reshape(-1, x.shape[-1]).contiguous(), w.dtype)
+                gw = _wgrad(g2, x.reshape(-1, x.shape[-1]).contiguous(), w.dtype)
         if ctx.has_b and ctx.needs_input_grad[2]:
             # a LayerNorm backward that consumed this output may have summed g
             # already (pcops_layernorm_bwd_colsum, attached to g); else one colsum
             pre = _take_sum(g)
-            gb = pre if pre is not None else colsum(g2.contiguous(), out_dtype=ctx.b_dtype)
+            gb = pre if pre is not None else colsum(g2, out_dtype=ctx.b_dtype)
         if gb is not None and ctx.b_dtype is not None and gb.dtype != ctx.b_dtype:
             gb = gb.to(ctx.b_dtype)
         return gx, gw, gb, None
@@ -168,11 +181,28 @@ class _nullctx:
         return False
 
 
+def _row_strided(g):
+    """g (rows, C) has unit column stride and rows ld >= C elements apart (ld % 8 == 0,
+    16-byte aligned): a channel slice of a wider gradient, usable in place."""
+    return (g.dim() == 2 and g.stride(1) == 1 and g.stride(0) >= g.shape[1] and g.stride(0) % 8 == 0
+            and g.data_ptr() % 16 == 0)
+
+
 def colsum(g, out_dtype=None):
     """g.sum(0) of a (rows, C) CUDA tensor (g's dtype unless out_dtype): pcops_colsum (fp32
     accumulation, deterministic order) when C % 8 == 0 or a row fold makes it so, torch's
-    reduction otherwise."""
+    reduction otherwise.  Rows evenly strided (a channel slice of a wider gradient) are
+    summed in place (pcops_colsum_ld)."""
     rows, C = g.shape
+    if (not g.is_contiguous() and C % 8 == 0 and g.dtype in _DT and _row_strided(g) and rows > 1
+            and g.is_cuda):
+        out = torch.empty(C, dtype=g.dtype if out_dtype is None else out_dtype, device=g.device)
+        wsb = lib().pcops_colsum_workspace_bytes(rows, C)
+        ws = _lib.Workspace.get(g.device, wsb)
+        with torch.cuda.device(g.device):
+            call("colsum", lib().pcops_colsum_ld, ptr(g), _dt(g), rows, C, g.stride(0), ptr(out),
+                 _DT[out.dtype], ptr(ws), wsb, stream_of(g))
+        return out
     if C % 8 and g.dtype in _DT and g.is_contiguous() and C < 64:
         # narrow outputs (conv_out: C = 3): torch's reduction ran on 4 blocks (~100 us);
         # fold k rows into one of k*C columns (k*C % 8 == 0), sum those in fp32, add the k groups
@@ -655,6 +685,8 @@ _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnost
 _GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
 # in_proj bias sums inside the attention backward passes (A/B switch)
 _ATTN_COLSUM = os.environ.get("PCOPS_ATTN_COLSUM", "1") != "0"
+_DEBUG_CONTIG = os.environ.get("PCOPS_DEBUG_CONTIG", "0") == "1"   # diagnostic: report _Linear operand copies
+_STRIDED_G = os.environ.get("PCOPS_STRIDED_G", "1") != "0"           # A/B switch: row-strided output gradients in place
 
 
 def _pos_tokens(pos):

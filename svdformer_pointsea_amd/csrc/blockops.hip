@@ -411,7 +411,7 @@ constexpr int kCsU = 8;
 
 template <int DT>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restrict__ g, long long rows, int C, int V,
-                                                             long long rpc, float *__restrict__ part) {
+                                                             long long rpc, float *__restrict__ part, long long ld) {
   __shared__ float red[4][64 * 8];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rw = 64 / V;                         // rows per wave step
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restr
 #pragma unroll
     for (int u = 0; u < kCsU; ++u) {
       const long long r = rb + u * step;
-      ld8c<DT>(t[u], g, (r < r1 ? r : rb) * C + col);
+      ld8c<DT>(t[u], g, (r < r1 ? r : rb) * ld + col);
     }
 #pragma unroll
     for (int u = 0; u < kCsU; ++u) {
@@ -924,8 +924,14 @@ extern "C" int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, l
 
 extern "C" int pcops_colsum(const void *g, int g_dtype, long long rows, int C, void *out, int out_dtype,
                             void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream) {
-  if (rows < 0 || C <= 0 || !dt_ok(g_dtype) || !dt_ok(out_dtype) || !out) return PCOPS_ERR_INVALID;
-  if (C % 8) return PCOPS_ERR_UNSUPPORTED;
+  return pcops_colsum_ld(g, g_dtype, rows, C, C, out, out_dtype, workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcops_colsum_ld(const void *g, int g_dtype, long long rows, int C, long long ld, void *out,
+                               int out_dtype, void *workspace, unsigned long long workspace_bytes,
+                               pcops_stream_t stream) {
+  if (rows < 0 || C <= 0 || ld < C || !dt_ok(g_dtype) || !dt_ok(out_dtype) || !out) return PCOPS_ERR_INVALID;
+  if (C % 8 || ld % 8) return PCOPS_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (rows == 0) {
     if (hipMemsetAsync(out, 0, (size_t)C * (out_dtype == 0 ? 4 : 2), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
@@ -940,9 +946,9 @@ extern "C" int pcops_colsum(const void *g, int g_dtype, long long rows, int C, v
   const dim3 grid(chunks, C / 8 / V);
   float *part = (float *)workspace;
   if (g_dtype == 0)
-    hipLaunchKernelGGL(colsum_partial_kernel<0>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part);
+    hipLaunchKernelGGL(colsum_partial_kernel<0>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part, ld);
   else
-    hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part);
+    hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part, ld);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, out, out_dtype, C,
                      nullptr, C, nullptr);
   PC_CHECK_LAUNCH();

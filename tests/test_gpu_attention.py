@@ -836,3 +836,47 @@ def test_attention_bwd_colsum(dev, B, H, Lq, Lk, E, packed, bf):
         ref = g1.double().reshape(-1, g1.shape[-1]).sum(0)
         bound = 2e-6 * g1.double().abs().reshape(-1, g1.shape[-1]).sum(0) + 1e-6
         assert ((s1.double() - ref).abs() <= bound).all(), (s1.double() - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("rows,C,ld,dtype", [(65536, 1024, 2048, torch.bfloat16), (16384, 128, 256, torch.bfloat16),
+                                             (999, 64, 72, torch.float32), (4096, 512, 1024, torch.float32)])
+def test_colsum_row_strided(dev, rows, C, ld, dtype):
+    """pcops_colsum_ld on a channel slice of a wider matrix: bitwise the contiguous colsum of the same
+    values, and within the fp32 accumulation bound of float64."""
+    from svdformer_pointsea_amd.attention import colsum
+
+    wide = torch.randn(rows, ld, generator=torch.Generator().manual_seed(rows + C)).to(dev, dtype)
+    g = wide[:, ld - C:]
+    assert not g.is_contiguous()
+    out = colsum(g, out_dtype=torch.float32)
+    ref = colsum(g.contiguous(), out_dtype=torch.float32)
+    assert torch.equal(out, ref)
+    exact = g.double().sum(0)
+    assert ((out.double() - exact).abs() <= 2e-6 * g.double().abs().sum(0) + 1e-6).all()
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_linear_sliced_output_gradient(dev, monkeypatch, amp):
+    """A Linear whose output is concatenated with another tensor gets a row-strided gradient
+    view: the in-place path (GEMMs with a leading dimension, pcops_colsum_ld) matches the
+    contiguous-copy path."""
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(3)
+    x = torch.randn(8, 2048, 256, device=dev)
+    w = torch.randn(512, 256, device=dev) * 0.05
+    b = torch.randn(512, device=dev) * 0.1
+    other = torch.randn(8, 2048, 384, device=dev)
+
+    def run(strided):
+        monkeypatch.setattr(A, "_STRIDED_G", strided)
+        xs, ws, bs = [t.clone().requires_grad_(True) for t in (x, w, b)]
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = A._Linear.apply(xs, ws, bs, bs.dtype)
+            out = torch.cat([other.to(y.dtype), y], -1)
+        (out.float() ** 2).sum().backward()
+        return xs.grad, ws.grad, bs.grad
+
+    ref, got = run(False), run(True)
+    for a, r in zip(got, ref):
+        torch.testing.assert_close(a, r, rtol=1e-2 if amp else 1e-5, atol=1e-3 if amp else 1e-5)
