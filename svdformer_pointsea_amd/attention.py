@@ -79,7 +79,7 @@ def _wgrad(g2, x2, wdt):
         # fixed-order sum of the slices (pcops_sum_rows) stays a few MB
         S = max(S, min(512, (1 << _WGRAD_SMALL_LOG2) // (Cout * Cin)))
         S = 1 << (S.bit_length() - 1)
-    while S > 1 and (T % S or T // S < (1024 if S > 16 else 2048)):
+    while S > 1 and (T % S or T // S < (1024 if S > 16 else _WGRAD_MINK)):
         S //= 2
     if S == 1 or g2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16:
         return (g2.t() @ x2).to(wdt)
@@ -678,6 +678,7 @@ _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switc
 _WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switch: split-K weight gradients
 _WGRAD_SMALL = os.environ.get("PCOPS_WGRAD_SMALL", "1") != "0"    # A/B switch: more split-K slices for small weights
 _WGRAD_SMALL_LOG2 = int(os.environ.get("PCOPS_WGRAD_SMALL_LOG2", "20"))  # partial elements aimed at (log2)
+_WGRAD_MINK = int(os.environ.get("PCOPS_WGRAD_MINK", "2048"))   # tokens per split-K slice at least (S <= 16)
 _PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
 _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnostic: fused sums in side-stream blocks too
 # linear11's bias sum inside the GELU backward (A/B switch); the sum reaches the

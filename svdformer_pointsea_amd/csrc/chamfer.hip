@@ -367,9 +367,16 @@ __global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
   __shared__ long long acc[kGTargets * 3];
   __shared__ int flags[kGTargets];
   __shared__ float red[kGThreads / 64];
-  const int b = blockIdx.y, tid = threadIdx.x;
-  const bool dir = (int)blockIdx.x >= parts0;
-  const int part = dir ? blockIdx.x - parts0 : blockIdx.x;
+  // 1-D grid, XCD-contiguous: consecutive logical blocks -- the parts of one (batch,
+  // direction), which all rescan the same source indices -- are dispatched to the same
+  // XCD (hardware block h runs on XCD h % 8), so the rescans hit that XCD's L2 instead of
+  // each XCD fetching the cloud from HBM
+  const int per = parts0 + parts1, total = (int)gridDim.x;
+  int L = blockIdx.x;
+  if ((total & 7) == 0) L = (L & 7) * (total >> 3) + (L >> 3);
+  const int b = L / per, x = L - b * per, tid = threadIdx.x;
+  const bool dir = x >= parts0;
+  const int part = dir ? x - parts0 : x;
   const int parts = dir ? parts1 : parts0;
   const int NA = dir ? M : N, NT = dir ? N : M;
   const float *S = (dir ? xyz2 : xyz1) + (size_t)b * NA * 3;
@@ -527,8 +534,8 @@ extern "C" int pcops_chamfer_backward(const float *xyz1, const float *xyz2, int 
       return p;
     };
     const int p0 = parts_for(M), p1 = parts_for(N);
-    hipLaunchKernelGGL(chamfer_grad_seg_kernel, dim3(p0 + p1, B), dim3(kGThreads), 0, s, xyz1, xyz2, N, M, graddist1,
-                       graddist2, idx1, idx2, gradxyz1, gradxyz2, p0, p1);
+    hipLaunchKernelGGL(chamfer_grad_seg_kernel, dim3((unsigned)((long)(p0 + p1) * B)), dim3(kGThreads), 0, s, xyz1,
+                       xyz2, N, M, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, p0, p1);
     PC_CHECK_LAUNCH();
     return PCOPS_OK;
   }

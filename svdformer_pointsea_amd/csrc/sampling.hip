@@ -216,6 +216,75 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
   FPS_STAMP_FLUSH
 }
 
+// One wave per cloud (small clouds): each lane holds R = T / 64 reference threads (r = lane * R + j,
+// so lane order is r order), PPL = R * PPT slots ordered by (j, i) -- the reference thread's k = tref +
+// T * i -- so "lowest lane with the max, then its first slot" is the reference's tie order (smallest
+// r, then smallest k).  A round is the sweep + one DPP wave max + the first-slot search + readlanes:
+// no LDS, no barrier.  Measured (B = 32, tools/fps_bench.py, profiles/r3_fps_wave_ab.txt): 512 -> 128
+// 0.471 -> 0.406 us/round, 1024 -> 256 equal, 2048 -> 512 0.577 -> 0.830 (the one wave's sweep of 32
+// slots is VALU-bound where 8 waves split it), so it runs only up to 8 slots per lane (<= 512 points).
+template <int PPL>
+__global__ __launch_bounds__(64) void fps_wave_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
+                                                      int R, int PPT, int *__restrict__ idx) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const float *p = xyz + (size_t)b * N * 3;
+  int *out = idx + (size_t)b * M;
+  constexpr int kNeverBits = 0xBF800000;  // -1.0f
+  float px[PPL], py[PPL], pz[PPL];
+  int tmp[PPL];
+#pragma unroll
+  for (int s = 0; s < PPL; ++s) {
+    const int j = s / PPT, i = s - j * PPT;  // PPT is uniform; s, j, i compile-time per slot only when PPT is
+    const int r = lane * R + j;
+    const int k = (int)bitrev_bits((unsigned)r, L) + T * i;
+    if (j < R && r < T && k < N) {
+      px[s] = p[3 * k];
+      py[s] = p[3 * k + 1];
+      pz[s] = p[3 * k + 2];
+      const float mag = sqd3(px[s], py[s], pz[s]);
+      tmp[s] = ((double)mag <= 1e-3) ? kNeverBits : fbits(1e10f);  // sampling_gpu.cu:100-101
+    } else {
+      px[s] = py[s] = pz[s] = 0.f;
+      tmp[s] = kNeverBits;
+    }
+  }
+  const float x0 = p[0], y0 = p[1], z0 = p[2];
+  float ox = x0, oy = y0, oz = z0;
+  if (lane == 0 && M > 0) out[0] = 0;
+  for (int jr = 1; jr < M; ++jr) {
+    int best = kNeverBits;
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) {
+      int d = fbits(sqd3(px[s] - ox, py[s] - oy, pz[s] - oz));
+      if constexpr (PPL >= 16) asm volatile("" : "+v"(d));  // scalar chains (see fps_reg_kernel)
+      tmp[s] = min(d, tmp[s]);
+      best = max(best, tmp[s]);
+    }
+    const int wmax = wave_max_i32(best);
+    const uint64_t tied = __ballot(best == wmax);
+    const int wl = (int)__builtin_ctzll(tied);
+    int b0 = PPL - 1, b1 = PPL - 1;
+#pragma unroll
+    for (int s = PPL - 2; s >= 0; s -= 2) {
+      b0 = (tmp[s] == wmax) ? s : b0;
+      if (s >= 1) b1 = (tmp[s - 1] == wmax) ? s - 1 : b1;
+    }
+    const int wbi = __builtin_amdgcn_readlane(min(b0, b1), wl);
+    int k;
+    if (wmax != kNeverBits) {
+      ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[wbi]), wl));
+      oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[wbi]), wl));
+      oz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[wbi]), wl));
+      const int j = wbi / PPT;
+      k = (int)bitrev_bits((unsigned)(wl * R + j), L) + T * (wbi - j * PPT);
+    } else {  // no valid point at all: the reference's dists_i[0] == 0
+      ox = x0, oy = y0, oz = z0;
+      k = 0;
+    }
+    if (lane == 0) out[jr] = k;
+  }
+}
+
 struct __align__(16) FpsSlot {
   float d, x, y, z;
   int k;
@@ -394,6 +463,28 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
   const int nthreads = T < 64 ? 64 : T;
   const int ppt = (N + T - 1) / T;  // points per reference thread
   hipStream_t s = (hipStream_t)stream;
+  {
+    // small clouds: one wave per cloud when its lanes hold <= PCOPS_FPS_WAVE slots (0: never)
+    static const int wave_cap = [] {
+      const char *e = getenv("PCOPS_FPS_WAVE");
+      return e ? atoi(e) : 8;
+    }();
+    const int R = T >= 64 ? T / 64 : 1;
+    const int ppl = R * ppt;
+#define FPS_WAVE_CASE(P)                                                                                     \
+  if (ppl <= P) {                                                                                            \
+    hipLaunchKernelGGL((fps_wave_kernel<P>), dim3(B), dim3(64), 0, s, xyz, N, M, T, L, R, ppt, idx);        \
+    PC_CHECK_LAUNCH();                                                                                       \
+    return PCOPS_OK;                                                                                         \
+  }
+    if (ppl <= wave_cap) {
+      FPS_WAVE_CASE(8)
+      FPS_WAVE_CASE(16)
+      FPS_WAVE_CASE(24)
+      FPS_WAVE_CASE(32)   // larger register arrays spill (PPL 40: 496 B of scratch per lane)
+    }
+#undef FPS_WAVE_CASE
+  }
   if (ppt <= kFpsMaxPPT) {
     // clouds with > 16 points per reference thread use 2 hardware threads per
     // reference thread (1024 threads, 4 waves / SIMD).  Up to 16 the 8-wave

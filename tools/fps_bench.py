@@ -1,5 +1,5 @@
 """FPS launch times (HIP events) at the step's shapes, B = 32: us per round.
-PCOPS_FPS_PRUNE=0 in the environment selects the full-sweep kernels (A/B)."""
+PCOPS_FPS_WAVE=0 in the environment keeps small clouds on the 8-wave block kernel (A/B)."""
 import os
 import sys
 
@@ -10,9 +10,10 @@ from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample  # noqa
 
 dev = torch.device("cuda", 0)
 g = torch.Generator(device="cpu").manual_seed(0)
-tag = "prune=" + os.environ.get("PCOPS_FPS_PRUNE", "1") + " nt=" + os.environ.get("PCOPS_FPS_PRUNE_NT", "512")
+tag = "wave=" + os.environ.get("PCOPS_FPS_WAVE", "32")
 for B, N, M, kind in [(32, 16384, 2048, "gauss"), (32, 16384, 2048, "surface"), (16, 8192, 2048, "surface"),
-                      (32, 2304, 512, "surface"), (32, 4096, 1024, "gauss")]:
+                      (32, 2304, 512, "surface"), (32, 4096, 1024, "gauss"), (32, 2048, 512, "gauss"),
+                      (32, 2048, 256, "gauss"), (32, 512, 128, "gauss"), (32, 1024, 256, "gauss")]:
     x = torch.randn(B, N, 3, generator=g)
     if kind == "surface":  # points on ellipsoid surfaces, like the PCN / ShapeNet gt clouds
         x = x / x.norm(dim=-1, keepdim=True) * torch.tensor([0.4, 0.25, 0.15])

@@ -96,8 +96,8 @@ run_stage() {
       done ;;
     avail) timeout -k 10 60 rocprofv3 --list-avail > "$OUT/avail.txt" 2>&1 ;;
     knn) timeout -k 10 120 python tools/knn_bench.py > "$OUT/knn_bench.txt" 2>&1 ;;
-    fps_ab)   # FPS times per env group in $FPS_AB ("A=1;A=0"), default pruned vs full sweep
-      IFS=';' read -ra groups <<< "${FPS_AB:-PCOPS_FPS_PRUNE=0;PCOPS_FPS_PRUNE=1}"
+    fps_ab)   # FPS times per env group in $FPS_AB ("A=1;A=0"), default block vs one-wave kernel
+      IFS=";" read -ra groups <<< "${FPS_AB:-PCOPS_FPS_WAVE=0;PCOPS_FPS_WAVE=32}"
       for g in "${groups[@]}"; do
         echo "== $g" >> "$OUT/fps_bench.txt"
         env $g timeout -k 10 120 python tools/fps_bench.py >> "$OUT/fps_bench.txt" 2>&1 || return 1
