@@ -296,6 +296,159 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
   }
 }
 
+// ---------------------------------------------------------------- screened on MFMA
+// The same screen with e(t) = |t|^2 - 2 a.t formed by the fp32 matrix cores: per wave 32 queries
+// (B operand, one per lane pair: column j = lane & 31) against 32-target tiles (A operand, row
+// i = target), K = 4 over t' = (x, y, z, |t|^2) and a' = (-2a, 1): two v_mfma_f32_32x32x2_f32 per
+// 1024 pairs.  A lane then holds 16 of its query's 32 e values per tile (rows 8g + 4h + c); four
+// tiles (128 targets, one slot's range) go through one v_min3 chain, one v_permlane32_swap with the
+// other half and the VALU kernel's keep / prune logic (the two halves of a lane pair run it
+// identically; the h = 0 lane re-derives and writes) -- the bookkeeping per 32-target sub-tile had
+// made this form VALU-bound again.  Per pair: 4 MFMA MACs + ~1/2 VALU op instead of 3 fma + 1/2
+// min on the VALU.  Margin: any fp32 evaluation
+// order of the 4-term sum errs by <= ~4u (|t|^2 + 2|a||t|) <= 16u (Tm^2 + |a| Tm), the eps below,
+// plus an absolute floor for flushed denormal products.
+typedef float f32x16m __attribute__((ext_vector_type(16)));
+constexpr int kSubM = 128;  // targets per keep test / slot: four 32 x 32 MFMA tiles
+
+__global__ __launch_bounds__(kThreads) void chamfer_mfma_kernel(const float *__restrict__ xyz1,
+                                                                const float *__restrict__ xyz2, int N, int M,
+                                                                float *__restrict__ dist1, float *__restrict__ dist2,
+                                                                int *__restrict__ idx1, int *__restrict__ idx2,
+                                                                int blocks_dir0) {
+  const int b = blockIdx.y;
+  const bool dir = (int)blockIdx.x >= blocks_dir0;
+  const int bx = dir ? blockIdx.x - blocks_dir0 : blockIdx.x;
+  const int NA = dir ? M : N, NT = dir ? N : M;
+  const float *A = (dir ? xyz2 : xyz1) + (size_t)b * NA * 3;
+  const float *T = (dir ? xyz1 : xyz2) + (size_t)b * NT * 3;
+  float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
+  int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
+  if (NT <= 0) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, w = tid >> 6;
+  const int qi = bx * (kThreads / 2) + w * 32 + (lane & 31);
+  const int qc = qi < NA ? qi : NA - 1;
+  const float ax = A[3 * qc], ay = A[3 * qc + 1], az = A[3 * qc + 2];
+  const float b1 = h ? -2.f * ay : -2.f * ax;  // B[k][j]: k = h (first MFMA), 2 + h (second)
+  const float b2 = h ? 1.f : -2.f * az;
+  const float an = (ax * ax + ay * ay) + az * az;
+  const float anorm = sqrtf(an);
+  float mine = INFINITY, slack = INFINITY;
+  float cm[kSlots];
+  int cs[kSlots];
+  bool over = !(an < INFINITY);
+#pragma unroll
+  for (int c = 0; c < kSlots; ++c) {
+    cm[c] = INFINITY;
+    cs[c] = -1;
+  }
+
+  __shared__ float2 txz[kTile], tyw[kTile];
+  __shared__ float tmax_s[kThreads / 64];
+  float eps_t2 = 0.f;
+  for (int t0 = 0; t0 < NT; t0 += kTile) {
+    const int cnt = min(kTile, NT - t0);
+    float lmax = 0.f;
+    for (int e = tid; e < kTile; e += kThreads) {
+      float2 xz = make_float2(0.f, 0.f), yw = make_float2(0.f, INFINITY);  // padding: e = +inf
+      if (e < cnt) {
+        const float *src = T + (size_t)(t0 + e) * 3;
+        const float x = src[0], y = src[1], z = src[2];
+        const float n2 = (x * x + y * y) + z * z;
+        xz = make_float2(x, z);
+        yw = make_float2(y, n2);
+        lmax = fmaxf(lmax, n2);
+      }
+      txz[e] = xz;
+      tyw[e] = yw;
+    }
+    lmax = wave_max_f32(lmax);
+    if ((tid & 63) == 0) tmax_s[tid >> 6] = lmax;
+    __syncthreads();
+#pragma unroll
+    for (int ww = 0; ww < kThreads / 64; ++ww) eps_t2 = fmaxf(eps_t2, tmax_s[ww]);
+    const float tm = sqrtf(eps_t2);
+    const float eps = 16.f * kU * (eps_t2 + anorm * tm) + 1e-35f;
+    slack = screen_slack(mine, an, eps);
+    const int nsub = (cnt + kSubM - 1) / kSubM;
+    for (int sb = 0; sb < nsub; ++sb) {
+      // kSubM / 32 independent 32 x 32 tiles, then one keep test for the kSubM targets
+      const float2 *src = (h ? tyw : txz) + sb * kSubM + (lane & 31);
+      float2 v[kSubM / 32];
+#pragma unroll
+      for (int u = 0; u < kSubM / 32; ++u) v[u] = src[32 * u];
+      f32x16m acc[kSubM / 32];
+#pragma unroll
+      for (int u = 0; u < kSubM / 32; ++u) {
+        acc[u] = f32x16m{};
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].x, b1, acc[u], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kSubM / 32; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u].y, b2, acc[u], 0, 0, 0);
+      float m = INFINITY;
+#pragma unroll
+      for (int u = 0; u < kSubM / 32; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) m = fminf(fminf(m, acc[u][r]), acc[u][r + 1]);
+      const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+      m = fminf(__uint_as_float(pr[0]), __uint_as_float(pr[1]));
+      const int sub0 = t0 + sb * kSubM;
+      if (m <= mine + slack) {  // rare: this sub-tile may hold the argmin
+        if (m < mine) {
+          mine = m;
+          slack = screen_slack(mine, an, eps);
+#pragma unroll
+          for (int c = 0; c < kSlots; ++c)
+            if (cs[c] >= 0 && cm[c] > mine + slack) cs[c] = -1;  // prune
+        }
+        bool placed = false;
+#pragma unroll
+        for (int c = 0; c < kSlots; ++c) {
+          if (!placed && cs[c] < 0) {
+            cs[c] = sub0;
+            cm[c] = m;
+            placed = true;
+          }
+        }
+        over = over || !placed;
+      }
+    }
+    __syncthreads();
+  }
+  if (h || qi >= NA) return;
+  // exact re-derivation with the reference expression (chamfer_screen_kernel's)
+  float best = INFINITY;
+  int bk = 0;
+  if (!over) {
+#pragma unroll
+    for (int c = 0; c < kSlots; ++c) {
+      if (cs[c] < 0) continue;
+      const int k0 = cs[c], k1 = min(k0 + kSubM, NT);
+      for (int k = k0; k < k1; ++k) {
+        const float d = sqd3(T[3 * k] - ax, T[3 * k + 1] - ay, T[3 * k + 2] - az);
+        if (d < best || (d == best && k < bk)) {
+          best = d;
+          bk = k;
+        }
+      }
+    }
+  }
+  if (over || !(best < INFINITY)) {  // full direct scan (overflow, non-finite data)
+    best = INFINITY;
+    bk = 0;
+    for (int k = 0; k < NT; ++k) {
+      const float d = sqd3(T[3 * k] - ax, T[3 * k + 1] - ay, T[3 * k + 2] - az);
+      if (d < best) {
+        best = d;
+        bk = k;
+      }
+    }
+  }
+  dist[qi] = best < INFINITY ? best : sqd3(T[3 * bk] - ax, T[3 * bk + 1] - ay, T[3 * bk + 2] - az);
+  idx[qi] = bk;
+}
+
 // own terms: grad_self[j] = 2 g_j (x_j - y_idx(j)), both directions
 __global__ void chamfer_grad_own_kernel(const float *__restrict__ xyz1, const float *__restrict__ xyz2, int B, int N,
                                         int M, const float *__restrict__ gd1, const float *__restrict__ gd2,
@@ -483,6 +636,21 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
     const char *e = getenv("PCOPS_CHAMFER_SCREEN");
     return !(e && e[0] == '0');
   }();
+  // PCOPS_CHAMFER_MFMA: 0 = the VALU screen only, 1 (default) = the MFMA screen for the launches
+  // the VALU screen runs at Q = 1 (B = 32, 2048^2: 0.071 -> 0.054 ms), 2 = everywhere (16384^2 it
+  // loses: 1.65 -> 1.82 ms -- the Q = 4 VALU screen is at the VALU issue rate, the MFMA form at
+  // about half the fp32 matrix rate with 104 VGPRs / 4 waves per SIMD; profiles/r3_chamfer_mfma_ab.txt)
+  static const int mfma = [] {
+    const char *e = getenv("PCOPS_CHAMFER_MFMA");
+    return e ? atoi(e) : 1;
+  }();
+  if (screen && (mfma == 2 || (mfma == 1 && Q == 1))) {
+    const int m0 = (N + kThreads / 2 - 1) / (kThreads / 2), m1 = (M + kThreads / 2 - 1) / (kThreads / 2);
+    hipLaunchKernelGGL(chamfer_mfma_kernel, dim3(m0 + m1, B), dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2,
+                       idx1, idx2, m0);
+    PC_CHECK_LAUNCH();
+    return PCOPS_OK;
+  }
   if (screen && Q == 4)
     hipLaunchKernelGGL(chamfer_screen_kernel<4>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1,
                        idx2, b0);
