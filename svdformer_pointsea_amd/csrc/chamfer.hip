@@ -300,8 +300,8 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
 // The same screen with e(t) = |t|^2 - 2 a.t formed by the fp32 matrix cores: per wave 32 queries
 // (B operand, one per lane pair: column j = lane & 31) against 32-target tiles (A operand, row
 // i = target), K = 4 over t' = (x, y, z, |t|^2) and a' = (-2a, 1): two v_mfma_f32_32x32x2_f32 per
-// 1024 pairs.  A lane then holds 16 of its query's 32 e values per tile (rows 8g + 4h + c); four
-// tiles (128 targets, one slot's range) go through one v_min3 chain, one v_permlane32_swap with the
+// 1024 pairs.  A lane then holds 16 of its query's 32 e values per tile (rows 8g + 4h + c); two
+// tiles (64 targets, one slot's range) go through one v_min3 chain, one v_permlane32_swap with the
 // other half and the VALU kernel's keep / prune logic (the two halves of a lane pair run it
 // identically; the h = 0 lane re-derives and writes) -- the bookkeeping per 32-target sub-tile had
 // made this form VALU-bound again.  Per pair: 4 MFMA MACs + ~1/2 VALU op instead of 3 fma + 1/2
@@ -309,8 +309,8 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
 // order of the 4-term sum errs by <= ~4u (|t|^2 + 2|a||t|) <= 16u (Tm^2 + |a| Tm), the eps below,
 // plus an absolute floor for flushed denormal products.
 typedef float f32x16m __attribute__((ext_vector_type(16)));
-constexpr int kSubM = 128;  // targets per keep test / slot: four 32 x 32 MFMA tiles
 
+template <int kSubM>   // targets per keep test / slot: kSubM / 32 MFMA tiles (default 64)
 __global__ __launch_bounds__(kThreads) void chamfer_mfma_kernel(const float *__restrict__ xyz1,
                                                                 const float *__restrict__ xyz2, int N, int M,
                                                                 float *__restrict__ dist1, float *__restrict__ dist2,
@@ -637,17 +637,35 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
     return !(e && e[0] == '0');
   }();
   // PCOPS_CHAMFER_MFMA: 0 = the VALU screen only, 1 (default) = the MFMA screen for the launches
-  // the VALU screen runs at Q = 1 (B = 32, 2048^2: 0.071 -> 0.054 ms), 2 = everywhere (16384^2 it
-  // loses: 1.65 -> 1.82 ms -- the Q = 4 VALU screen is at the VALU issue rate, the MFMA form at
-  // about half the fp32 matrix rate with 104 VGPRs / 4 waves per SIMD; profiles/r3_chamfer_mfma_ab.txt)
+  // the VALU screen runs at Q = 1 (B = 32, 2048^2: 0.071 -> 0.048 ms; PCN step 51.88 -> 51.58 ms,
+  // same box), 2 = everywhere: at 16384^2 alone it ties the Q = 4 VALU screen (1.67 vs 1.69 ms), in
+  // the step it measured 0.4-0.8 ms slower (it shares the matrix cores with the concurrent GEMMs /
+  // attention of the other stream); profiles/r3_chamfer_mfma_ab.txt
   static const int mfma = [] {
     const char *e = getenv("PCOPS_CHAMFER_MFMA");
     return e ? atoi(e) : 1;
   }();
   if (screen && (mfma == 2 || (mfma == 1 && Q == 1))) {
     const int m0 = (N + kThreads / 2 - 1) / (kThreads / 2), m1 = (M + kThreads / 2 - 1) / (kThreads / 2);
-    hipLaunchKernelGGL(chamfer_mfma_kernel, dim3(m0 + m1, B), dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2,
-                       idx1, idx2, m0);
+    // PCOPS_CHAMFER_MFMA_SUB: 32 / 64 / 128 / 256 targets per keep test (A/B).  64 measured best
+    // (B = 32, 16384^2 / 2048^2: 32 -> 1.80 / 0.051 ms, 64 -> 1.64-1.67 / 0.047-0.049, 128 -> 1.84 /
+    // 0.053, 256 -> 2.30 / 0.104): 72 VGPRs (7 waves / SIMD) against 104 / 136 at 128 / 256
+    static const int sub = [] {
+      const char *e = getenv("PCOPS_CHAMFER_MFMA_SUB");
+      return e ? atoi(e) : 64;
+    }();
+    if (sub == 32)
+      hipLaunchKernelGGL(chamfer_mfma_kernel<32>, dim3(m0 + m1, B), dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1,
+                         dist2, idx1, idx2, m0);
+    else if (sub == 64)
+      hipLaunchKernelGGL(chamfer_mfma_kernel<64>, dim3(m0 + m1, B), dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1,
+                         dist2, idx1, idx2, m0);
+    else if (sub == 256)
+      hipLaunchKernelGGL(chamfer_mfma_kernel<256>, dim3(m0 + m1, B), dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1,
+                         dist2, idx1, idx2, m0);
+    else
+      hipLaunchKernelGGL(chamfer_mfma_kernel<128>, dim3(m0 + m1, B), dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1,
+                         dist2, idx1, idx2, m0);
     PC_CHECK_LAUNCH();
     return PCOPS_OK;
   }
