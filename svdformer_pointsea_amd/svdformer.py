@@ -499,6 +499,21 @@ class SDG(nn.Module):
         return coarse.repeat(1, r, 1) + O_L
 
 
+_IMG_STREAM = _os.environ.get("PCOPS_IMG_STREAM", "1") != "0"   # A/B switch: image branch on its own stream
+
+
+class _NoFork:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+    @staticmethod
+    def join(*tensors):
+        return tensors[0] if len(tensors) == 1 else tensors
+
+
 class SVFNet(nn.Module):
     """SVDFormer.py:106-173: shape-view fusion encoder (image + point branches)."""
 
@@ -529,10 +544,16 @@ class SVFNet(nn.Module):
     def forward(self, points, depth):
         batch_size, _, N = points.size()
         depth = depth.contiguous(memory_format=torch.channels_last)
-        # stem conv (1 -> 16) on libpcops under bf16 autocast, each BN + ReLU fused
-        f_v = run_sequential(self.img_feature_extractor, depth, conv3x3).view(batch_size, 3, -1).transpose(1, 2)
-        f_v = f_v.contiguous()
+        # the image branch (convs + BatchNorm, no GEMM) and the point branch (FPS, kNN, grouping,
+        # PCSA: launches of 32-512 blocks) are independent until viewattn: with PCOPS_IMG_STREAM
+        # the image branch runs on a third stream beside the point branch (and the local
+        # encoder on the first side stream), forward and backward
+        with fork(points.device, lane=2, inputs=(depth,)) if _IMG_STREAM else _NoFork() as br:
+            # stem conv (1 -> 16) on libpcops under bf16 autocast, each BN + ReLU fused
+            f_v = run_sequential(self.img_feature_extractor, depth, conv3x3).view(batch_size, 3, -1).transpose(1, 2)
+            f_v = f_v.contiguous()
         f_p = self.point_feature_extractor(points)
+        f_v = br.join(f_v)
         view_point = self.view_point.expand(batch_size, 3, 3)
         view_feature = self.posmlp(view_point).permute(2, 0, 1)
         f_v_ = self.viewattn(torch.cat([f_v, f_p.repeat(1, 1, f_v.size(2))], 1), view_feature)
