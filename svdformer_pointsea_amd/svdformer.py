@@ -499,7 +499,9 @@ class SDG(nn.Module):
         return coarse.repeat(1, r, 1) + O_L
 
 
-_IMG_STREAM = _os.environ.get("PCOPS_IMG_STREAM", "1") != "0"   # A/B switch: image branch on its own stream
+# PCOPS_IMG_STREAM=1: the image branch on a third stream beside the point branch.  Off: same-box PCN
+# A/B, 5 runs each, 51.01-53.04 ms (mean 52.1, bimodal run to run) against 51.64-51.91 (mean 51.78)
+_IMG_STREAM = _os.environ.get("PCOPS_IMG_STREAM", "0") == "1"
 
 
 class _NoFork:
