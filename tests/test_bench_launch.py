@@ -41,3 +41,21 @@ def test_world_size_must_match_gpus():
     assert out.returncode != 0
     assert "--gpus 4 but WORLD_SIZE=2" in out.stderr
     assert out.stdout.strip() == ""     # no JSON line with a wrong n_gpus
+
+
+def test_attention_work_parses_both_call_forms():
+    """bench.kernel_work reads (B, H, Lq, Lk, D, dtype) from the plain attention entries and from the
+    *_colsum ones, which carry extra output pointers before B (the position counts from the end)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    B, H, Lq, Lk, D = 2, 8, 2048, 1024, 64
+    strides = (0,) * 12
+    tail = (B, H, Lq, Lk, D, 0.125, 1) + strides + (None, 0, None)   # ..., workspace, bytes, stream
+    for lead in (7, 8):   # pcops_attention_bwd_dq_delta / _dq_delta_colsum
+        assert bench.kernel_work("attention bwd dq", (None,) * lead + tail)[0] == 2.0 * B * H * Lq * Lk * D
+    for lead in (7, 9):   # pcops_attention_bwd_dkv / _dkv_colsum
+        assert bench.kernel_work("attention bwd dkv", (None,) * lead + tail)[0] == 8.0 * B * H * Lq * Lk * D
+    fwd = (None,) * 5 + (B, H, Lq, Lk, D, 0.125, 1) + strides + (None,)
+    work, unit, _, bound = bench.kernel_work("attention forward", fwd)
+    assert work == 4.0 * B * H * Lq * Lk * D and unit == "TFLOP/s" and bound == "mfma"
