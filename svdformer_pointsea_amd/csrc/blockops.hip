@@ -481,6 +481,60 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float *__restr
   }
 }
 
+// Opt-in variant of colsum_final_kernel (PCOPS_COLSUM_FINAL_CW=16, untimed): CW columns x (1024 / CW)
+// row groups per block with 8 loads in flight per thread -- twice the blocks and half the serial
+// loads per thread of the 32-column form at CW = 16 (a ~1024-chunk final is latency-bound on 16-96
+// blocks).  Fixed order for a given CW.
+template <int CW>
+__global__ __launch_bounds__(1024) void colsum_final_cw_kernel(const float *__restrict__ part, int chunks, int C,
+                                                               void *__restrict__ out, int odt, int split,
+                                                               void *__restrict__ out2, int split2,
+                                                               void *__restrict__ out3) {
+  constexpr int G = 1024 / CW, U = 8;
+  __shared__ float red[G][CW + 1];
+  const int cl = threadIdx.x % CW, grp = threadIdx.x / CW;
+  const int col = blockIdx.x * CW + cl;
+  float s = 0.f;
+  if (col < C)
+    for (int k0 = grp; k0 < chunks; k0 += U * G) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * G;
+        v[u] = part[(long long)(k < chunks ? k : k0) * C + col];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += (k0 + u * G < chunks) ? v[u] : 0.f;
+    }
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && col < C) {
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < G; ++i) tot += red[i][cl];
+    if (col < split)
+      st(out, odt, col, tot);
+    else if (col < split2)
+      st(out2, odt, col - split, tot);
+    else
+      st(out3, odt, col - split2, tot);
+  }
+}
+
+void launch_colsum_final(const float *part, int chunks, int C, void *out, int odt, int split, void *out2,
+                         int split2, void *out3, hipStream_t s) {
+  static const int cw = [] {
+    const char *e = getenv("PCOPS_COLSUM_FINAL_CW");
+    return e ? atoi(e) : 32;
+  }();
+  if (cw == 16)
+    hipLaunchKernelGGL(colsum_final_cw_kernel<16>, dim3((C + 15) / 16), dim3(1024), 0, s, part, chunks, C, out, odt,
+                       split, out2, split2, out3);
+  else
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, out, odt, split,
+                       out2, split2, out3);
+}
+
 // GELU backward (exact erf form, torch's GeluBackward expression in fp32) fused
 // with the column sum of its output -- the bias gradient of the Linear whose
 // output the GELU consumed -- in colsum_partial_kernel's launch shape:
@@ -845,8 +899,7 @@ int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a
   ln_dispatch<LnBwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p, (dy32 ? 1 : 0) | (dy16 ? 2 : 0), blocks,
                       ln_bwd_rpw(rows));
   const int np = dsum ? 3 : 2;
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((np * C + 31) / 32), dim3(1024), 0, s, part, blocks, np * C,
-                     (void *)dgamma, 0, C, (void *)dbeta, 2 * C, (void *)dsum);
+  launch_colsum_final(part, blocks, np * C, (void *)dgamma, 0, C, (void *)dbeta, 2 * C, (void *)dsum, s);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
@@ -908,8 +961,7 @@ extern "C" int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, l
       hipLaunchKernelGGL((gelu_bwd_partial_kernel<0, true>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc, part);
     else
       hipLaunchKernelGGL((gelu_bwd_partial_kernel<1, true>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc, part);
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, (void *)dsum, 0,
-                       C, nullptr, C, nullptr);
+    launch_colsum_final(part, chunks, C, (void *)dsum, 0, C, nullptr, C, nullptr, s);
   } else {
     if (dtype == 0)
       hipLaunchKernelGGL((gelu_bwd_partial_kernel<0, false>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc,
@@ -949,8 +1001,7 @@ extern "C" int pcops_colsum_ld(const void *g, int g_dtype, long long rows, int C
     hipLaunchKernelGGL(colsum_partial_kernel<0>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part, ld);
   else
     hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, s, g, rows, C, V, rpc, part, ld);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, out, out_dtype, C,
-                     nullptr, C, nullptr);
+  launch_colsum_final(part, chunks, C, out, out_dtype, C, nullptr, C, nullptr, s);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
