@@ -272,7 +272,7 @@ def kernel_work(name, a):
 # libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
             "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
-            "chamfer_3D.forward": "chamfer_(nn|screen)_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
+            "chamfer_3D.forward": "chamfer_(nn|screen|mfma)_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
             "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",
             "colsum": ("colsum", "colsum_partial"),
             "transpose_add": "transpose_add", "pcsa_forward": "pcsa_fwd", "pcsa_backward": "pcsa_bwd",
@@ -386,7 +386,7 @@ class Workload:
             return partial
         from svdformer_pointsea_amd.data import seprate_point_cloud
         n = gt.shape[1]
-        return seprate_point_cloud(gt, n, [n // 4, 3 * n // 4], generator=generator)[0]
+        return seprate_point_cloud(gt, n, [n // 4, 3 * n // 4], generator=generator, want_crop=False)[0]
 
     def gt_pyramid(self, gt):
         """The loss's gt FPS chain (n_out -> 2048 -> 256); depends on gt only."""

@@ -685,7 +685,10 @@ _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnost
 # Linear's backward through _attach_sum / _take_sum (stream-safe hand-off)
 _GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
 # in_proj bias sums inside the attention backward passes (A/B switch)
-_ATTN_COLSUM = os.environ.get("PCOPS_ATTN_COLSUM", "1") != "0"
+# the in-pass bias sums exist only in the v2/v3 bf16 kernels: the PCOPS_ATTN_V1 A/B
+# switch (libpcops returns UNSUPPORTED for *_colsum there) takes the plain passes
+_ATTN_COLSUM = (os.environ.get("PCOPS_ATTN_COLSUM", "1") != "0"
+                and os.environ.get("PCOPS_ATTN_V1", "0") != "1")
 _DEBUG_CONTIG = os.environ.get("PCOPS_DEBUG_CONTIG", "0") == "1"   # diagnostic: report _Linear operand copies
 _STRIDED_G = os.environ.get("PCOPS_STRIDED_G", "1") != "0"           # A/B switch: row-strided output gradients in place
 

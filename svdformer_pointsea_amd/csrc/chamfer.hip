@@ -506,8 +506,13 @@ __global__ void chamfer_grad_partner_kernel(const float *__restrict__ xyz1, cons
 // (the reference's expressions, chamfer3D.cu:155-174).  Pass 1 finds the largest finite |c| of
 // the block's targets; the scale 2^sh makes every term and every possible sum (at most NA
 // terms) fit int64, and pass 2 adds round(c * 2^sh) with LDS 64-bit integer atomics: exact and
-// order-independent.  Error per sum <= NA * 2^-(sh+1) ~ max|c| * 2^-48, then one rounding to
-// fp32 (the reference's fp32 atomic sum errs by ~2^-24 of the sum of |c| and varies run to run).
+// order-independent.  Each term is rounded to 2^-sh, so the sum of target j's n_j terms errs by
+// at most n_j * 2^-(sh+1) = n_j * 2^(e+lg-63) (|c| < 2^e over the whole BLOCK, NA < 2^lg): an
+// ABSOLUTE resolution set by the block's largest term, ~max|c| * 2^-48 per term at NA = 16384 --
+// a target whose own terms are far below an outlier of its block gets that absolute bound, not
+// fp32-relative precision (tests/test_gpu_pointops.py::test_chamfer_backward_outlier_block_bound).
+// Then one rounding to fp32 (the reference's fp32 atomic sum errs by ~2^-24 of the sum of |c|
+// and varies run to run).
 // Non-finite terms set per-component flags (+inf / -inf / NaN, atomicOr): the sum is then
 // +-inf or NaN from the flags alone, again whatever the order.
 constexpr int kGThreads = 512;

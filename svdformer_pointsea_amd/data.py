@@ -36,14 +36,18 @@ def _pack(points, order, start, count, n_max):
     return out * keep.unsqueeze(-1).to(out.dtype)
 
 
-def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=False, generator=None):
+def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=False, generator=None,
+                        want_crop=True):
     """utils/helpers.py:62-123 -> (input_data, crop_data).
 
     crop: int, or [lo, hi] for a per-sample random crop size (then both parts
     are FPS-subsampled to 2048, as the reference does).  fixed_points: None
     (random unit centre per sample), one (3,) point or a list to sample from.
     `generator` (optional, a torch.Generator on xyz's device) replaces the
-    reference's global `random` / `torch.randn` draws for reproducible runs."""
+    reference's global `random` / `torch.randn` draws for reproducible runs.
+    want_crop=False returns (input_data, None) without the crop part's FPS: the
+    train loop discards it (core/train_55.py:150 `partial, _ = ...`), FPS draws
+    no random numbers, so input_data is unchanged."""
     B, n, c = xyz.shape
     assert n == num_points
     assert c == 3
@@ -76,6 +80,8 @@ def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=
         hi = int(crop[1])
         if not padding_zeros:
             input_data = _pack(xyz, order, num_crop, n - num_crop, n - int(crop[0]))
+        if not want_crop:
+            return fps_subsample(input_data.contiguous(), 2048), None
         crop_data = _pack(xyz, order, torch.zeros_like(num_crop), num_crop, hi)
         # the two FPS launches (B workgroups each) run side by side
         crop_data = crop_data.contiguous()
@@ -86,5 +92,7 @@ def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=
     k = int(crop)
     if not padding_zeros:
         input_data = torch.gather(xyz, 1, order[:, k:].unsqueeze(-1).expand(B, n - k, 3))
+    if not want_crop:
+        return input_data.contiguous(), None
     crop_data = torch.gather(xyz, 1, order[:, :k].unsqueeze(-1).expand(B, k, 3))
     return input_data.contiguous(), crop_data.contiguous()

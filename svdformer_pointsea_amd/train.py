@@ -467,6 +467,21 @@ def load_checkpoint_state(ckpt, model, optimizer, fp=None, prefix="module."):
             else:
                 flat_state[k] = v.clone() if torch.is_tensor(v) else v   # never alias the source's step
     (cur,) = optimizer.state_dict()["param_groups"]
+    # the live optimizer's implementation switches win over the saved ones
+    # (checkpoint_state writes the per-tensor defaults): a capturable / fused
+    # flat optimizer stays one, and its step is placed on the device by
+    # torch's loader because the group it sees says capturable
     group = {**group, "params": cur["params"]}
+    for k in ("fused", "capturable", "foreach", "differentiable"):
+        if k in cur:
+            group[k] = cur[k]
+    live = optimizer.param_groups[0]
+    lr_tensors = {k: live[k] for k in ("lr", "initial_lr") if torch.is_tensor(live.get(k))}
     optimizer.load_state_dict({"state": {cur["params"][0]: flat_state} if flat_state else {},
                                "param_groups": [group]})
+    # a captured graph reads the LR through the tensor it was captured with:
+    # keep that tensor and write the saved value into it
+    live = optimizer.param_groups[0]
+    for k, t in lr_tensors.items():
+        t.fill_(float(live[k]))
+        live[k] = t

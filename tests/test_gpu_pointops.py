@@ -99,6 +99,34 @@ def test_fps_edge_cases_bitexact(dev, kind):
     np.testing.assert_array_equal(got, O.furthest_point_sample(x, M))
 
 
+@pytest.mark.parametrize("kind", ["tiled512", "tiled256", "zeros512", "all_zero512", "n513", "tiled64"])
+def test_fps_wave_kernel_edge_cases_bitexact(dev, kind):
+    """The one-wave kernel (clouds of <= 512 points, fps_wave_kernel) on the inputs
+    that stress its re-implemented tie order and skip rule: padded
+    partials with duplicated points and more samples than distinct points,
+    skipped near-origin points, an all-zero cloud, and N = 513 (the first size
+    past it)."""
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
+
+    rng = np.random.default_rng(100 + len(kind))
+    if kind == "tiled512":
+        x, M = _tiled(rng, 3, 90, 512), 128
+    elif kind == "tiled256":
+        x, M = _tiled(rng, 2, 40, 256), 200
+    elif kind == "tiled64":
+        x, M = _tiled(rng, 2, 9, 64), 64
+    elif kind == "zeros512":
+        x, M = (rng.random((2, 512, 3)) - 0.5).astype(np.float32), 400
+        x[:, -100:] = 0.0
+        x[:, 10:30] = 1e-2   # |p|^2 = 3e-4 <= 1e-3: skipped
+    elif kind == "all_zero512":
+        x, M = np.zeros((2, 512, 3), np.float32), 32
+    else:
+        x, M = _tiled(rng, 2, 200, 513), 300
+    got = furthest_point_sample(T(x, dev), M).cpu().numpy()
+    np.testing.assert_array_equal(got, O.furthest_point_sample(x, M))
+
+
 def test_fps_full_size_properties(dev):
     """B=32, 16384 -> 2048 (the loss FPS): size-independent properties."""
     from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
@@ -262,6 +290,38 @@ def test_chamfer_backward_deterministic(dev, case):
         # ... and the oracle's sequential fp32 sums within their own rounding (not for the hub's 3000-term sum)
         if case != "hub":
             np.testing.assert_allclose(got[fin], ora[fin], rtol=1e-5, atol=1e-6 * scale)
+
+
+def test_chamfer_backward_outlier_block_bound(dev):
+    """one large partner term sets the fixed-point scale of every target in
+    its block, so a target with small terms gets absolute, not relative, resolution.
+    The per-target bound is n_j * 2^(e + lg - 63) (n_j partner terms, every finite
+    |c| of the block < 2^e, NA < 2^lg sources) plus the final fp32 rounding; checked
+    against the float64 sum of the same fp32 terms, target by target, with a 1e6
+    upstream gradient on one far source next to O(1) ones."""
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    rng = np.random.default_rng(77)
+    a = (rng.random((1, 2100, 3)) - 0.5).astype(np.float32)
+    b = (rng.random((1, 1900, 3)) - 0.5).astype(np.float32)
+    a[0, 5] = (60.0, -40.0, 25.0)          # far source: its partner term is ~1e8
+    w1 = rng.random(a.shape[:2]).astype(np.float32)
+    w2 = rng.random(b.shape[:2]).astype(np.float32)
+    w1[0, 5] = 1e6
+    at, bt = T(a, dev).requires_grad_(True), T(b, dev).requires_grad_(True)
+    d1, d2, i1, i2 = chamfer_3DDist()(at, bt)
+    ((d1 * T(w1, dev)).sum() + (d2 * T(w2, dev)).sum()).backward()
+    i1, i2 = i1.cpu().numpy(), i2.cpu().numpy()
+    r1, r2 = _chamfer_grad64(a, b, w1, w2, i1, i2)
+    for got, ref, S, Tc, gS, iS in ((at.grad.cpu().numpy(), r1, b, a, w2, i2),
+                                     (bt.grad.cpu().numpy(), r2, a, b, w1, i1)):
+        c = (2 * gS[..., None]).astype(np.float32) * (S - np.take_along_axis(Tc, iS[..., None].astype(np.int64), 1))
+        e = int(np.frexp(np.abs(c).max())[1])                 # every |c| < 2^e
+        lg = int(S.shape[1]).bit_length()                     # NA < 2^lg
+        n = np.bincount(iS[0].astype(np.int64), minlength=Tc.shape[1])[None, :, None]
+        tol = n * 2.0 ** (e + lg - 63) + 2.0 ** -24 * np.abs(ref) + 1e-30
+        err = np.abs(got.astype(np.float64) - ref)
+        assert (err <= tol).all(), float((err / tol).max())
 
 
 def _chamfer_grad64(a, b, w1, w2, i1, i2):

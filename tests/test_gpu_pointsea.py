@@ -87,3 +87,22 @@ def test_seprate_point_cloud_matches_per_sample_loop(dev):
         ref_cr = fps_subsample(pts[0, idx[:k]].unsqueeze(0).contiguous(), 2048)
         assert torch.equal(inp[b:b + 1], ref_in)
         assert torch.equal(cr[b:b + 1], ref_cr)
+
+
+def test_seprate_point_cloud_without_crop_same_input(dev):
+    """want_crop=False (the train loop's `partial, _ = ...`, core/train_55.py:150)
+    skips the crop part's FPS and returns the same input cloud, bitwise: FPS draws
+    no random numbers, so the generator stream is unchanged."""
+    from svdformer_pointsea_amd.data import seprate_point_cloud
+
+    _, gt = synth_55(4, 12, dev)
+    n = gt.shape[1]
+    crop = [n // 4, 3 * n // 4]
+    a, ca = seprate_point_cloud(gt, n, crop, generator=torch.Generator(device=dev).manual_seed(7))
+    b, cb = seprate_point_cloud(gt, n, crop, generator=torch.Generator(device=dev).manual_seed(7), want_crop=False)
+    assert ca is not None and cb is None
+    assert torch.equal(a, b)
+    for k in (n // 2,):   # fixed crop size: the gather path
+        a, _ = seprate_point_cloud(gt, n, k, generator=torch.Generator(device=dev).manual_seed(8))
+        b, cb = seprate_point_cloud(gt, n, k, generator=torch.Generator(device=dev).manual_seed(8), want_crop=False)
+        assert cb is None and torch.equal(a, b)

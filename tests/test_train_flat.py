@@ -259,3 +259,77 @@ def test_checkpoint_from_capturable_tensor_lr_optimizer_loads_into_plain_adam():
         opt.step()
     for (n, pa), (_, pc) in zip(a.named_parameters(), c.named_parameters()):
         torch.testing.assert_close(pc.data, pa.data, rtol=1e-6, atol=1e-7, msg=n)
+
+
+def test_checkpoint_roundtrip_keeps_tensor_lr_and_switches():
+    """reloading this repo's own checkpoint (reference layout: float lr,
+    default switches) into bench.py's kind of flat optimizer (tensor LR a captured
+    graph reads, explicit implementation switches) keeps that LR tensor object --
+    the saved value written into it -- and the live switches, and then steps
+    exactly like the optimizer that wrote the checkpoint."""
+    from svdformer_pointsea_amd.train import checkpoint_state, load_checkpoint_state
+
+    torch.manual_seed(7)
+    a = _Net3()
+    b = copy.deepcopy(a)
+    fa = FlatParams(a, "cpu", bf16=False)
+    oa = torch.optim.Adam([fa.master()], lr=torch.tensor(1e-2), foreach=False)
+    for step in range(2):
+        x = torch.randn(2, 4, 3, 5, generator=torch.Generator().manual_seed(step))
+        fa.zero_grad()
+        fa.forward(x).backward()
+        oa.step()
+    ck = checkpoint_state(a, oa, fa)
+    fb = FlatParams(b, "cpu", bf16=False)
+    lr_t = torch.tensor(0.5)
+    ob = torch.optim.Adam([fb.master()], lr=lr_t, foreach=False)
+    load_checkpoint_state(ck, b, ob, fb)
+    g = ob.param_groups[0]
+    assert g["lr"] is lr_t and float(lr_t) == float(torch.tensor(1e-2))
+    assert g["foreach"] is False
+    x = torch.randn(2, 4, 3, 5, generator=torch.Generator().manual_seed(9))
+    for f, o in ((fa, oa), (fb, ob)):
+        f.zero_grad()
+        f.forward(x).backward()
+        o.step()
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(pa.data, pb.data), n
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_checkpoint_roundtrip_capturable_flat_optimizer_gpu():
+    """The same round trip into a capturable, tensor-LR flat Adam on the GPU
+    (bench.py's optimizer): capturable stays on, the step stays on the device,
+    the captured LR tensor is kept, and the next step equals the writer's."""
+    from svdformer_pointsea_amd.train import checkpoint_state, load_checkpoint_state
+
+    dev = "cuda"
+    torch.manual_seed(8)
+    a = _Net3().to(dev)
+    b = copy.deepcopy(a)
+    fa = FlatParams(a, dev, bf16=False)
+    oa = torch.optim.Adam([fa.master()], lr=torch.tensor(1e-2, device=dev), capturable=True, foreach=False)
+    for step in range(2):
+        x = torch.randn(2, 4, 3, 5, generator=torch.Generator().manual_seed(step)).to(dev)
+        fa.zero_grad()
+        fa.forward(x).backward()
+        oa.step()
+    ck = checkpoint_state(a, oa, fa)
+    fb = FlatParams(b, dev, bf16=False)
+    lr_t = torch.tensor(0.5, device=dev)
+    ob = torch.optim.Adam([fb.master()], lr=lr_t, capturable=True, foreach=False)
+    load_checkpoint_state(ck, b, ob, fb)
+    g = ob.param_groups[0]
+    assert g["capturable"] is True and g["lr"] is lr_t
+    (st,) = ob.state.values()
+    assert st["step"].is_cuda
+    x = torch.randn(2, 4, 3, 5, generator=torch.Generator().manual_seed(9)).to(dev)
+    for f, o in ((fa, oa), (fb, ob)):
+        f.zero_grad()
+        f.forward(x).backward()
+        o.step()
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(pa.data, pb.data), n
