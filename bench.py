@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--dist-selftest", action="store_true",
                     help="initialise an RCCL process group even at N=1 (exercises the collective path "
                          "and its graph capture on a one-GPU box)")
+    ap.add_argument("--no-input-prefetch", action="store_true",
+                    help="ShapeNet-55: crop + FPS the step's own input at its head (A/B of the input prefetch)")
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the fp32 PCN train step and the PointSea ShapeNet-55 train step reported beside "
                          "the headline (N = 1 only)")
@@ -340,6 +342,49 @@ def kernel_table(spans):
     return rows
 
 
+def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
+    """The line's kernel fields for one train leg: `roofline` (the dominant libpcops
+    call group), `fps_us_per_round`, `composite_fps_knn_chamfer` and the per-call
+    `kernels` table (HIP-event times per step, frac, PMC traffic ratio)."""
+    out = {}
+    timed = {k: r for k, r in rows.items() if "frac" in r}
+    if not timed:
+        return out
+    dom_key = max(timed, key=lambda k: timed[k]["ms"])
+    d = timed[dom_key]
+    out["roofline"] = {"kernel": dom_key, "bound": d["bound"], "achieved": round(d["achieved"], 2),
+                       "peak": d["peak"] / (1e12 if d["unit"] == "TFLOP/s" else 1e9), "unit": d["unit"],
+                       "frac": round(d["frac"], 4),
+                       "traffic": pmc_traffic(pmc_json, dom_key, d["name"]),
+                       "traffic_source": os.path.relpath(pmc_json, ROOT) if pmc_json else None,
+                       "avg_launch_ms": round(d["ms"] / d["launches"], 4),
+                       "work_per_launch": d["work"] / d["launches"]}
+    # FPS is M-1 serially dependent rounds: its honest figure is time per round
+    fps = {}
+    for e0, e1, a in spans.get("furthest_point_sampling", []):
+        f = fps.setdefault(f"B{a[1]} {a[2]}->{a[3]}", [0, 0.0, a[3]])
+        f[0] += 1
+        f[1] += e0.elapsed_time(e1)
+    out["fps_us_per_round"] = {k: round(v[1] * 1e3 / v[0] / max(1, v[2] - 1), 3) for k, v in fps.items()}
+    group = [r for r in timed.values() if r["name"] in ("furthest_point_sampling", "knn", "chamfer_3D.forward")]
+    if group:
+        out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) / sum(r["ms"] for r in group), 4)
+
+    def pmc_row(k, r):
+        t = pmc_traffic(pmc_json, k, r["name"])
+        if t is None or not r.get("work") or r.get("unit") != "GB/s":
+            return {}
+        return {"pmc_traffic_ratio": round(t / (r["work"] / r["launches"]), 3)}
+
+    out["kernels"] = {k: {"launches_per_step": r["launches"] / span_steps,
+                          "ms_per_step": round(r["ms"] / span_steps, 4),
+                          "share": round(r["ms"] / span_steps / step_ms, 4),
+                          **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {}),
+                          **pmc_row(k, r)}
+                      for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
+    return out
+
+
 # ------------------------------------------------------------------ workloads
 class Workload:
     """One of the two train steps: the reference loop it restates, its model,
@@ -478,11 +523,19 @@ def fp32_forward_loss(wl, model, partial, gt, device, steps, use_graph, batch=16
             fwd()
         run = gr.replay
     torch.cuda.synchronize()
+    # PCOPS_TRACE_MARKS=configs1: spin kernels around these timed steps (tools/trace_window.py)
+    marks = os.environ.get("PCOPS_TRACE_MARKS") == "configs1"
+    if marks:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         run()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    if marks:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     model.train(was_training)
     return {"config": "BASELINE configs[1]: SVDFormer forward + get_loss, PCN shapes, fp32", "batch": batch,
             "steps": steps, "ms_per_step": round(dt * 1e3, 3), "samples_per_s": round(batch / dt, 2),
@@ -619,6 +672,15 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
     progress(f"[{tag}] {wl.name} B={batch} {'bf16' if amp else 'fp32'}: {L.nparams} parameters; eager warm-up")
     sync = [BucketedAllReduce(fp, world, bucket_mb=args.bucket_mb) if use_dist and args.overlap == "auto" else None]
 
+    # ShapeNet-55's input (seprate_point_cloud: crop + a 16-CU FPS, ~2 ms) depends on
+    # gt and the crop draws only, not on the model: each step crops and FPS-samples
+    # the NEXT step's input on a third stream beside its own forward/backward, as a
+    # data loader's prefetch would (one crop per step, every one inside a timed
+    # step; the first step's comes from before the clock).  --no-input-prefetch
+    # puts it back at the head of the step's critical path (A/B).
+    prefetch = crop_rng is not None and not args.no_input_prefetch
+    staged = [wl.inputs(partial, gt, crop_rng)] if prefetch else None
+
     def fwd_bwd():
         fp.zero_grad()
         fp.refresh()
@@ -626,7 +688,12 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
         # stream beside the whole forward pass (FPS occupies B CUs)
         with _lib.fork(device, lane=1, inputs=(gt,)) as br:
             gts = wl.gt_pyramid(gt)
-        inp = wl.inputs(partial, gt, crop_rng)
+        if prefetch:
+            inp = staged[0].clone()   # this step's own buffer: the staged one is refilled below
+            with _lib.fork(device, lane=2, inputs=(gt,)) as bn:
+                nxt = wl.inputs(partial, gt, crop_rng)
+        else:
+            inp = wl.inputs(partial, gt, crop_rng)
         depth = wl.images(inp)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=not use_graph):
             pcds = fp.forward(inp, depth)
@@ -636,6 +703,8 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
             sync[0].finish()   # the bucketed all-reduces were issued during backward
         else:
             fp.collect()
+        if prefetch:
+            staged[0].copy_(bn.join(nxt))
         loss_acc.add_(loss.detach())  # logged without a host sync
 
     def grad_sync():
@@ -786,10 +855,15 @@ def extra_leg(args, name, batch, amp, device, steps):
     """A second train-step figure beside the headline (rank 0, N = 1)."""
     wl = Workload(name)
     setup_tunableop(args.tunableop, name, 0)
-    leg = train_leg(args, wl, batch, amp, steps, 2, device, 1, 0, False, False, name + ("" if amp else "-fp32"))
+    leg = train_leg(args, wl, batch, amp, steps, 2, device, 1, 0, False, not args.no_kernel_timing,
+                    name + ("" if amp else "-fp32"))
     out = {"workload": wl.desc, "batch": batch, "dtype": "bf16" if amp else "f32", "steps": steps,
            "ms_per_step": round(leg.ms_per_step, 3), "samples_per_s": round(batch * 1e3 / leg.ms_per_step, 2),
            "execution": "hip_graph" if leg.use_graph else "eager"}
+    if name == "pointsea" and amp:
+        out["input_prefetch"] = not args.no_input_prefetch
+    # the leg's own libpcops kernel table (HIP events of its eager timing steps)
+    out.update(kernel_summary(kernel_table(leg.spans), leg.spans, leg.span_steps, leg.ms_per_step, args.pmc_json))
     del leg
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -887,43 +961,7 @@ def main():
                        "points_out": wl.n_out, "params": nparams,
                        "parallelism": f"dp{world}" if world > 1 else "single"},
         }
-        timed = {k: r for k, r in rows.items() if "frac" in r}
-        if timed:
-            dom_key = max(timed, key=lambda k: timed[k]["ms"])
-            d = timed[dom_key]
-            out["roofline"] = {"kernel": dom_key, "bound": d["bound"], "achieved": round(d["achieved"], 2),
-                               "peak": d["peak"] / (1e12 if d["unit"] == "TFLOP/s" else 1e9), "unit": d["unit"],
-                               "frac": round(d["frac"], 4),
-                               "traffic": pmc_traffic(args.pmc_json, dom_key, d["name"]),
-                               "traffic_source": os.path.relpath(args.pmc_json, ROOT) if args.pmc_json else None,
-                               "avg_launch_ms": round(d["ms"] / d["launches"], 4),
-                               "work_per_launch": d["work"] / d["launches"]}
-            # FPS is M-1 serially dependent rounds: its honest figure is time per round
-            fps = {}
-            for e0, e1, a in spans.get("furthest_point_sampling", []):
-                f = fps.setdefault(f"B{a[1]} {a[2]}->{a[3]}", [0, 0.0, a[3]])
-                f[0] += 1
-                f[1] += e0.elapsed_time(e1)
-            out["fps_us_per_round"] = {k: round(v[1] * 1e3 / v[0] / max(1, v[2] - 1), 3) for k, v in fps.items()}
-            group = [r for r in timed.values() if r["name"] in ("furthest_point_sampling", "knn",
-                                                                 "chamfer_3D.forward")]
-            if group:
-                out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) /
-                                                         sum(r["ms"] for r in group), 4)
-            step_ms = elapsed * 1e3 / args.steps
-
-            def pmc_row(k, r):
-                t = pmc_traffic(args.pmc_json, k, r["name"])
-                if t is None or not r.get("work") or r.get("unit") != "GB/s":
-                    return {}
-                return {"pmc_traffic_ratio": round(t / (r["work"] / r["launches"]), 3)}
-
-            out["kernels"] = {k: {"launches_per_step": r["launches"] / span_steps,
-                                  "ms_per_step": round(r["ms"] / span_steps, 4),
-                                  "share": round(r["ms"] / span_steps / step_ms, 4),
-                                  **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {}),
-                                  **pmc_row(k, r)}
-                              for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
+        out.update(kernel_summary(rows, spans, span_steps, elapsed * 1e3 / args.steps, args.pmc_json))
         if fp32_leg is not None:
             out["fp32_forward_loss"] = fp32_leg
         out.update(extra)

@@ -48,6 +48,20 @@ run_stage() {
            find "$OUT/trace" -name '*kernel_trace.csv' -exec gzip -9 {} +   # keep the merge-back small
            [ $rc -eq 0 ] || tail -30 "$OUT/trace.err"
            return $rc ;;
+    trace_fp32|trace_c1|trace_ps)   # replay-only kernel trace of the fp32 train step / the configs[1] leg / PointSea
+      case "$1" in
+        trace_fp32) mk=1; tw=5; bargs="--fp32 --steps 5 --warmup 2 --no-extra-legs" ;;
+        trace_c1) mk=configs1; tw=3; bargs="--steps 6 --warmup 2 --no-extra-legs --no-kernel-timing" ;;
+        trace_ps) mk=1; tw=10; bargs="--model pointsea --steps 10 --warmup 3" ;;
+      esac
+      PCOPS_TRACE_MARKS=$mk timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$1" -o run -- \
+        python bench.py $bargs --no-cpu-baseline > "$OUT/$1.json" 2> "$OUT/$1.err"
+      rc=$?
+      [ $rc -eq 0 ] && python tools/trace_window.py "$(find "$OUT/$1" -name '*kernel_trace.csv' -print -quit)" $tw \
+        "$OUT/${1}_kernel_stats_replay.csv" > "$OUT/${1}_window.txt" 2>&1
+      find "$OUT/$1" -name '*kernel_trace.csv' -exec gzip -9 {} +
+      [ $rc -eq 0 ] || tail -30 "$OUT/$1.err"
+      return $rc ;;
     pmc_traffic)
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
         -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
