@@ -146,7 +146,7 @@ def synth_55(B, seed, device, n_gt=8192):
 # ------------------------------------------------------------------ roofline model
 # attention calls: B is followed by H, Lq, Lk, D, scale, dtype, 12 strides and 1 (forward) or 3 trailing
 # args, so its position counts from the end (the *_colsum entries carry extra pointers before B)
-ATTN_ARGS = {"attention forward": 20, "attention bwd dq": 22, "attention bwd dkv": 22}
+ATTN_ARGS = {"attention forward": 20, "attention bwd dq": 22, "attention bwd dkv": 22, "attention bwd": 22}
 
 
 def _attn_b(name, a):
@@ -162,6 +162,7 @@ def kernel_work(name, a):
       attention dq    2*BH*Lq*Lk*D FLOP (dQ only, delta = rowsum(dO*O) fused in; the S/dP recompute in this
                       pass is overhead, not credited -- FA2's 10*BH*Lq*Lk*D
                       total backward count)
+      attention bwd   10*BH*Lq*Lk*D FLOP (the one-call backward: delta, dK/dV storing dS, dQ = dS K)
       FPS             16 B per point-iteration, B*N*M of them (HBM model)
       Chamfer fwd     8 FLOP per pair, 2*B*N*M pairs (both directions)
       kNN             (2C+2) FLOP per (query, candidate) pair (distance part)
@@ -170,7 +171,7 @@ def kernel_work(name, a):
     if name in ATTN_ARGS:
         i = _attn_b(name, a)  # position of B; then H, Lq, Lk, D, scale, dtype
         BH, Lq, Lk, D, dt = a[i] * a[i + 1], a[i + 2], a[i + 3], a[i + 4], a[i + 6]
-        mult = {"attention forward": 4.0, "attention bwd dkv": 8.0, "attention bwd dq": 2.0}[name]
+        mult = {"attention forward": 4.0, "attention bwd dkv": 8.0, "attention bwd dq": 2.0, "attention bwd": 10.0}[name]
         return mult * BH * Lq * Lk * D, "TFLOP/s", MFMA_BF16_PEAK if dt == 1 else MFMA_F32_PEAK, "mfma"
     if name == "attention bwd delta":
         BH, Lq, D, dt = a[2] * a[3], a[4], a[5], a[6]
@@ -273,6 +274,7 @@ def kernel_work(name, a):
 
 # libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
+            "attention bwd": "attn_(delta2|dkv3|dqs)_kernel",
             "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
             "chamfer_3D.forward": "chamfer_(nn|screen|mfma)_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
             "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",
@@ -817,6 +819,20 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
     check_finite("the timed steps")
+    L.idle_issue_ms = None
+    if use_graph:
+        # host cost of issuing one step's graph replays against an IDLE GPU: separates
+        # the graph-launch cost of ~1.5 k nodes from queue back-pressure in host_issue
+        # (these replays are extra train steps, outside the clock)
+        idle = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            h0 = time.perf_counter()
+            step()
+            idle.append(time.perf_counter() - h0)
+        torch.cuda.synchronize()
+        check_finite("the idle-issue steps")
+        L.idle_issue_ms = 1e3 * sorted(idle)[1]
     if use_graph and kernel_timing:
         # ROCm torch refuses timing events inside a captured graph ("External
         # events are disallowed in rocm"), so the per-launch HIP events come
@@ -913,6 +929,7 @@ def main():
                     not args.no_kernel_timing, "headline")
     elapsed, spans, span_steps, sync = leg.elapsed, leg.spans, leg.span_steps, leg.sync
     use_graph, host_ms, nparams = leg.use_graph, leg.host * 1e3 / args.steps, leg.nparams
+    idle_issue_ms = leg.idle_issue_ms
 
     fp32_leg = None
     extra = {}
@@ -942,6 +959,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "host_issue_ms_per_step": host_ms,
+            "host_issue_idle_gpu_ms": None if idle_issue_ms is None else round(idle_issue_ms, 3),
             "execution": "hip_graph" if use_graph else "eager",
             "grad_sync": ("none (single GPU)" if not use_dist else
                           f"bucketed all-reduce from backward hooks ({len(sync.buckets)} buckets of "

@@ -229,6 +229,22 @@ int pcops_attention_bwd_dkv_colsum(const void *q, const void *k, const void *v, 
                                    long long q_srow, long long k_sb, long long k_sh, long long k_srow, long long v_sb,
                                    long long v_sh, long long v_srow, long long o_sb, long long o_sh, long long o_srow,
                                    void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+/* The whole backward in one call (models/model_utils.py:542-617, the autograd of
+ * nn.MultiheadAttention's attention core): dq, dk, dv, and -- when dq_colsum, dk_colsum
+ * and dv_colsum are all non-NULL (bf16 only) -- their per-head column sums as above.
+ * bf16 with D >= 96: the dK/dV pass also stores dS^T (bf16) into workspace and dQ = dS K
+ * is read back from it (no S / dP recompute; dQ bitwise equal to the two-pass form);
+ * otherwise the two-pass sequence.  workspace:
+ * pcops_attention_bwd_fused_workspace_bytes (includes the B*H x Lk x Lq bf16 dS^T
+ * buffer, rounded up, for bf16 D >= 96). */
+unsigned long long pcops_attention_bwd_fused_workspace_bytes(int B, int H, int Lq, int Lk, int D, int dtype);
+int pcops_attention_bwd_fused(const void *q, const void *k, const void *v, const void *o, const void *dout,
+                              const float *lse, void *dq, void *dk, void *dv, float *dq_colsum, float *dk_colsum,
+                              float *dv_colsum, int B, int H, int Lq, int Lk, int D, float scale, int dtype,
+                              long long q_sb, long long q_sh, long long q_srow, long long k_sb, long long k_sh,
+                              long long k_srow, long long v_sb, long long v_sh, long long v_srow, long long o_sb,
+                              long long o_sh, long long o_srow, void *workspace, unsigned long long workspace_bytes,
+                              pcops_stream_t stream);
 
 /* ---------------- attention-block glue (self_attention / cross_attention,
  * models/model_utils.py:584-617 and :542-582: the permute(2,0,1) / permute(1,2,0)

@@ -52,6 +52,8 @@ _SIGS = {
     "pcops_attention_bwd_dkv": (I, [P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
     "pcops_attention_bwd_dq_delta": (I, [P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
     "pcops_attention_bwd_colsum_workspace_bytes": (ULL, [I, I, I, I, I]),
+    "pcops_attention_bwd_fused_workspace_bytes": (ULL, [I, I, I, I, I, I]),
+    "pcops_attention_bwd_fused": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
     "pcops_attention_bwd_dq_delta_colsum": (I, [P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
     "pcops_attention_bwd_dkv_colsum": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
     "pcops_transpose_add": (I, [P, I, P, I, P, I, P, I, I, I, I, P]),

@@ -304,8 +304,27 @@ class AttentionCore(Function):
         dt = _DT[o.dtype]
         qp, kp, vp = _vptr(q_t, qw[1]), _vptr(k_t, kw[1]), _vptr(v_t, vw[1])
         want = ctx.want_sum
-        if (want is not None and any(want) and _ATTN_COLSUM and o.dtype == torch.bfloat16
-                and all(covered[i] == s.shape[-1] for i, s in enumerate(srcs))):
+        sum_ok = (want is not None and any(want) and _ATTN_COLSUM and o.dtype == torch.bfloat16
+                  and all(covered[i] == s.shape[-1] for i, s in enumerate(srcs)))
+        if o.dtype == torch.bfloat16 and hd >= 96 and _ATTN_FUSED:
+            # one call: delta, the dK/dV pass storing dS^T, dQ = dS K read back (no S / dP
+            # recompute; libpcops pcops_attention_bwd_fused), the bias sums when wanted
+            sums = ([torch.empty(s.shape[-1], dtype=torch.float32, device=o.device) for s in srcs]
+                    if sum_ok else None)
+            wsb = lib().pcops_attention_bwd_fused_workspace_bytes(B, heads, Lq, Lk, hd, dt)
+            ws = _lib.Workspace.get(o.device, wsb)
+            sp = ((_vptr(sums[qw[0]], qw[1]), _vptr(sums[kw[0]], kw[1]), _vptr(sums[vw[0]], vw[1]))
+                  if sums else (None, None, None))
+            with torch.cuda.device(o.device):
+                call("attention bwd", lib().pcops_attention_bwd_fused, qp, kp, vp, ptr(o), ptr(do), ptr(lse),
+                     _vptr(grads[qw[0]], qw[1]), _vptr(grads[kw[0]], kw[1]), _vptr(grads[vw[0]], vw[1]), *sp,
+                     B, heads, Lq, Lk, hd, float(scale), dt, *st, ptr(ws), wsb, stream_of(o))
+            if sums:
+                for g, dsum, w in zip(grads, sums, want):
+                    if w:
+                        _attach_sum(g, dsum)
+            return (None, *grads)
+        if sum_ok:
             # one fp32 sum per source column, written by the passes in window order
             sums = [torch.empty(s.shape[-1], dtype=torch.float32, device=o.device) for s in srcs]
             wsb = lib().pcops_attention_bwd_colsum_workspace_bytes(B, heads, Lq, Lk, hd)
@@ -687,6 +706,8 @@ _GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
 # in_proj bias sums inside the attention backward passes (A/B switch)
 # the in-pass bias sums exist only in the v2/v3 bf16 kernels: the PCOPS_ATTN_V1 A/B
 # switch (libpcops returns UNSUPPORTED for *_colsum there) takes the plain passes
+# bf16, head_dim >= 96: the one-call backward with dQ from the stored dS (A/B: PCOPS_ATTN_FUSED=0)
+_ATTN_FUSED = os.environ.get("PCOPS_ATTN_FUSED", "1") != "0"
 _ATTN_COLSUM = (os.environ.get("PCOPS_ATTN_COLSUM", "1") != "0"
                 and os.environ.get("PCOPS_ATTN_V1", "0") != "1")
 _DEBUG_CONTIG = os.environ.get("PCOPS_DEBUG_CONTIG", "0") == "1"   # diagnostic: report _Linear operand copies

@@ -1233,12 +1233,17 @@ __device__ __forceinline__ void dkv3_c(f32x16 (&Y1)[D / 32], f32x16 (&Y2)[D / 32
     }
 }
 
-template <int D, int OCC, bool CS>
+// DS: also store dS^T (bf16, the values C(j) multiplies -- the dQ pass's dS rounded the same
+// way) to dsT[bh][key][q] (ds_rows x ds_cols per head), for attn_dqs_kernel: dQ = dS K
+// without recomputing S and dP.  Keys >= Lk store 0 (their S would be exp2(-lse): the dQ
+// pass masks them).
+template <int D, int OCC, bool CS, bool DS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dkv3_kernel(
     const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K, const __bf16 *__restrict__ V,
     const __bf16 *__restrict__ dO, const float *__restrict__ lse, const float *__restrict__ delta,
     __bf16 *__restrict__ dK, __bf16 *__restrict__ dV, int Lq, int Lk, float scale, Strides st,
-    float *__restrict__ cpart_k, float *__restrict__ cpart_v) {
+    float *__restrict__ cpart_k, float *__restrict__ cpart_v, __bf16 *__restrict__ dsT, int ds_rows,
+    int ds_cols) {
   constexpr int NW = 4, RS = Img<D>::RS, TB = kKT * RS;  // TB: elements per tile slot
   constexpr int kCPT = kKT * D / 8 / (NW * 64);           // 16-B chunks per thread per tile
   static_assert(kKT * D / 8 % (NW * 64) == 0, "tile chunks must split evenly");
@@ -1338,8 +1343,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   int cur = 0, nxt = 1;  // slots of tiles t and t+1
   // one half step: [A(j+1) | B(j)] then C(j).  hq / hg: this half's Q / dO rows,
   // nq / ng: the next half's (unused when !NEXT); cl / cd: this half's row constants
+  __bf16 *ds_row = nullptr;  // this lane's key row of dS^T
+  if constexpr (DS) ds_row = dsT + ((long long)bh * ds_rows + ki) * ds_cols + 8 * h;
   auto half = [&](auto next_c, const __bf16 *hq, const __bf16 *hg, const __bf16 *nq, const __bf16 *ng,
-                  const float *cl, const float *cd, auto &&mid) {
+                  const float *cl, const float *cd, int qh0, auto &&mid) {
     constexpr bool NEXT = decltype(next_c)::value;
     bf16x8 qa[D / 16], ga[D / 16];
     if constexpr (NEXT) {
@@ -1353,6 +1360,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     bf16x8 va[D / 16], ka[D / 16];
     dkv3_ab<D, NEXT>(Sn, Gn, qa, ga, kf, vf, Sc, Gc, rc, sl2, pw, gw, va, ka, hq, hg);
     if constexpr (!(PCOPS_DKV3_ABL & 2)) dkv3_c<D>(Y1, Y2, va, ka, pw, gw);
+    if constexpr (DS) {
+      // lane (key, h) holds queries 8g + 4h + 0..3 (g = 0..3) as bf16 pairs gw[2g], gw[2g+1]:
+      // one permlane32 swap per pair of words gives each lane two runs of 8 queries
+      // (h = 0: queries 0-7 and 16-23, h = 1: 8-15 and 24-31), stored as 16 B each
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      unsigned w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = kv ? gw[i] : 0u;
+      const auto a0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+      const auto a1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+      const auto b0 = __builtin_amdgcn_permlane32_swap(w[4], w[6], false, false);
+      const auto b1 = __builtin_amdgcn_permlane32_swap(w[5], w[7], false, false);
+      *reinterpret_cast<u32x4 *>(ds_row + qh0) = (u32x4){a0[0], a1[0], a0[1], a1[1]};
+      *reinterpret_cast<u32x4 *>(ds_row + qh0 + 16) = (u32x4){b0[0], b1[0], b0[1], b1[1]};
+    }
     mid();
     Sc = Sn;
     Gc = Gn;
@@ -1362,20 +1384,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   for (; t + 1 < nt; ++t) {
     const __bf16 *cq = sq + cur * TB, *cg = sg + cur * TB;
     const float *cl = slse + cur * kKT, *cd = sdl + cur * kKT;
-    half(std::true_type{}, cq, cg, cq + 32 * RS, cg + 32 * RS, cl, cd, [&] {
+    half(std::true_type{}, cq, cg, cq + 32 * RS, cg + 32 * RS, cl, cd, t * kKT, [&] {
       store(nxt);
       load(t + 2);  // past the end: clamped rows, never stored
     });
     lds_barrier();
-    half(std::true_type{}, cq + 32 * RS, cg + 32 * RS, sq + nxt * TB, sg + nxt * TB, cl + 32, cd + 32, none);
+    half(std::true_type{}, cq + 32 * RS, cg + 32 * RS, sq + nxt * TB, sg + nxt * TB, cl + 32, cd + 32, t * kKT + 32,
+         none);
     cur = nxt;
     nxt = nxt == 2 ? 0 : nxt + 1;
   }
   {
     const __bf16 *cq = sq + cur * TB, *cg = sg + cur * TB;
     const float *cl = slse + cur * kKT, *cd = sdl + cur * kKT;
-    half(std::true_type{}, cq, cg, cq + 32 * RS, cg + 32 * RS, cl, cd, none);
-    half(std::false_type{}, cq + 32 * RS, cg + 32 * RS, cq, cg, cl + 32, cd + 32, none);
+    half(std::true_type{}, cq, cg, cq + 32 * RS, cg + 32 * RS, cl, cd, t * kKT, none);
+    half(std::false_type{}, cq + 32 * RS, cg + 32 * RS, cq, cg, cl + 32, cd + 32, t * kKT + 32, none);
   }
   store_Y<__bf16, D>(Y1, dV + st.v_off(bh), st.v_srow, k0w, Lk, 1.f);
   store_Y<__bf16, D>(Y2, dK + st.k_off(bh), st.k_srow, k0w, Lk, scale);
@@ -1388,6 +1411,138 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     lds_barrier();
     colsum_block<D, NW>(sc, cpart_v + row);
     colsum_block<D, NW>(sc + NW * D, cpart_k + row);
+  }
+}
+
+// ----------------------------------------------------------------- dQ from the stored dS (D >= 96)
+// delta = rowsum(dO o O) for the bf16 passes, in the fused-delta order of attn_dq2_kernel
+// (each lane half sums its d = 16 s + 8 h + e by fma in (s, e) order, then the halves are
+// added): the dK/dV pass runs first on this path and sees the same delta bitwise.
+template <int D>
+__global__ __launch_bounds__(256) void attn_delta2_kernel(const __bf16 *__restrict__ O, const __bf16 *__restrict__ dO,
+                                                          float *__restrict__ delta, int BH, int Lq, Strides st) {
+  const int l = lane_(), h = l >> 5;
+  const long long row = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (l & 31);
+  if (row >= (long long)BH * Lq) return;  // both halves of a row leave together
+  const int bh = (int)(row / Lq), q = (int)(row - (long long)bh * Lq);
+  const __bf16 *orow = O + st.o_off(bh) + (long long)q * st.o_srow + 8 * h;
+  const __bf16 *grow = dO + st.o_off(bh) + (long long)q * st.o_srow + 8 * h;
+  float part = 0.f;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const bf16x8 of = *reinterpret_cast<const bf16x8 *>(orow + 16 * s);
+    const bf16x8 gf = *reinterpret_cast<const bf16x8 *>(grow + 16 * s);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part = __builtin_fmaf((float)of[e], (float)gf[e], part);
+  }
+  const float dl = swap_halves_sum(part);
+  if (h == 0) delta[row] = dl;
+}
+
+// dQ = scale * dS K from the dS^T the dK/dV pass stored (attn_dkv3_kernel<.., DS>): 8 waves
+// x 32 queries per block, 64-key tiles of K (Img<D>) and of dS^T (keys x the block's 256
+// queries) double-buffered in LDS.  Per wave and tile the MFMAs are attn_dq2_kernel's
+// v_product calls in the same order with the same bf16 operands -- the B operand read from
+// the dS^T image by the same transposed-read pattern instead of converted from registers --
+// so dQ equals the recomputing pass's bitwise.  HBM-bound on the dS^T read (2 B per
+// (query, key)); it replaces 3 GEMM units of MFMA work (S, dP recomputed, dQ) by 1.
+constexpr int kDsRS = 256 + 32;  // dS^T image row stride (elements): conflict-free tr reads (tools/lds_banks.py)
+
+template <int D>
+__device__ __forceinline__ void v_product_ds(f32x16 (&Y)[D / 32], const __bf16 *kimg, const __bf16 *dimg) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int row0 = 16 * s + 4 * h + q;
+    const short4v blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(dimg + row0 * kDsRS + 16 * g + 4 * p));
+    const short4v bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(dimg + (row0 + 8) * kDsRS + 16 * g + 4 * p));
+    const bf16x8 b = __builtin_shufflevector(__builtin_bit_cast(bf16x4, blo), __builtin_bit_cast(bf16x4, bhi), 0, 1, 2,
+                                             3, 4, 5, 6, 7);
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      const int ch = 4 * db + 2 * g + (p >> 1), e = 4 * (p & 1);
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(kimg + img_off<D>(row0, ch) + e));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(kimg + img_off<D>(row0 + 8, ch) + e));
+      const bf16x8 a = __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1,
+                                               2, 3, 4, 5, 6, 7);
+      Y[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, Y[db], 0, 0, 0);
+    }
+  }
+#endif
+}
+
+template <int D, bool CS>
+__global__ __launch_bounds__(512) void attn_dqs_kernel(const __bf16 *__restrict__ K, const __bf16 *__restrict__ dsT,
+                                                       __bf16 *__restrict__ dQ, int Lq, int Lk, float scale, Strides st,
+                                                       int ds_rows, int ds_cols, float *__restrict__ cpart) {
+  constexpr int NW = 8, NT = NW * 64, RS = Img<D>::RS, KB = kKT * RS, SB = kKT * kDsRS;
+  constexpr int kKC = (kKT * D / 8 + NT - 1) / NT;  // K chunks per thread
+  constexpr int kDC = kKT * 32 / NT;                 // dS^T chunks per thread (64 rows x 32 chunks)
+  extern __shared__ __attribute__((aligned(16))) unsigned char dqs_smem[];
+  __bf16 *sk = reinterpret_cast<__bf16 *>(dqs_smem);  // [2][KB]
+  __bf16 *sd = sk + 2 * KB;                            // [2][SB]
+  int rb, bh;
+  xcd_block(rb, bh);
+  const int l = lane_(), w = threadIdx.x >> 6;
+  const int q0 = rb * (NW * 32) + w * 32;
+  const __bf16 *Kb = K + st.k_off(bh);
+  const __bf16 *Db = dsT + (long long)bh * ds_rows * ds_cols + rb * (NW * 32);
+  f32x16 Y[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) Y[db] = f32x16{};
+  bf16x8 kr[kKC], dr[kDC];
+  auto load = [&](int t) {
+    const int k0 = t * kKT;
+#pragma unroll
+    for (int c = 0; c < kKC; ++c) {
+      const int idx = threadIdx.x + c * NT;
+      const int row = idx / (D / 8), ch = idx % (D / 8);
+      const bool ok = (kKT * D / 8 % NT == 0 || idx < kKT * D / 8) && k0 + row < Lk;
+      kr[c] = ok ? *reinterpret_cast<const bf16x8 *>(Kb + (long long)(k0 + row) * st.k_srow + ch * 8) : bf16x8{};
+    }
+#pragma unroll
+    for (int c = 0; c < kDC; ++c) {
+      const int idx = threadIdx.x + c * NT;
+      dr[c] = *reinterpret_cast<const bf16x8 *>(Db + (long long)(k0 + (idx >> 5)) * ds_cols + (idx & 31) * 8);
+    }
+  };
+  auto store = [&](int slot) {
+#pragma unroll
+    for (int c = 0; c < kKC; ++c) {
+      const int idx = threadIdx.x + c * NT;
+      if (kKT * D / 8 % NT != 0 && idx >= kKT * D / 8) continue;
+      *reinterpret_cast<bf16x8 *>(sk + slot * KB + img_off<D>(idx / (D / 8), idx % (D / 8))) = kr[c];
+    }
+#pragma unroll
+    for (int c = 0; c < kDC; ++c) {
+      const int idx = threadIdx.x + c * NT;
+      *reinterpret_cast<bf16x8 *>(sd + slot * SB + (idx >> 5) * kDsRS + (idx & 31) * 8) = dr[c];
+    }
+  };
+  const int nt = (Lk + kKT - 1) / kKT;
+  load(0);
+  store(0);
+  lds_barrier();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) load(t + 1);
+    const __bf16 *ck = sk + cur * KB, *cd = sd + cur * SB + 32 * w;
+    v_product_ds<D>(Y, ck, cd);
+    v_product_ds<D>(Y, ck + 32 * RS, cd + 32 * kDsRS);
+    if (t + 1 < nt) {
+      store(cur ^ 1);
+      lds_barrier();
+    }
+  }
+  store_Y<__bf16, D>(Y, dQ + st.q_off(bh), st.q_srow, q0, Lq, scale);
+  if constexpr (CS) {
+    lds_barrier();  // every wave is past its last tile read
+    float *sc = reinterpret_cast<float *>(dqs_smem);
+    colsum_wave<D>(Y, scale, q0 + (l & 31) < Lq, sc, w);
+    lds_barrier();
+    colsum_block<D, NW>(sc, cpart + colsum_row(bh, rb, st.H, D));
   }
 }
 
@@ -1466,20 +1621,21 @@ int launch_dkv2_cfg(const void *q, const void *k, const void *v, const void *dou
   return PCOPS_OK;
 }
 
-template <int D, int OCC, bool CS>
+template <int D, int OCC, bool CS, bool DS = false>
 int launch_dkv3(const void *q, const void *k, const void *v, const void *dout, const float *lse, const float *delta,
                 void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s,
-                ColPart *cp) {
+                ColPart *cp, __bf16 *dsT = nullptr, int ds_rows = 0, int ds_cols = 0) {
   if ((long long)kKT * (st.q_srow > st.o_srow ? st.q_srow : st.o_srow) >= (1ll << 31)) return PCOPS_ERR_UNSUPPORTED;
   const size_t lds = 6ull * kKT * Img<D>::RS * sizeof(__bf16) + 6 * kKT * sizeof(float);
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv3_kernel<D, OCC, CS>,
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv3_kernel<D, OCC, CS, DS>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lk + 127) / 128, BH);
   if (cp) cp->nrb = grid.x;
-  hipLaunchKernelGGL((attn_dkv3_kernel<D, OCC, CS>), grid, dim3(256), lds, s, (const __bf16 *)q, (const __bf16 *)k,
-                     (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk, (__bf16 *)dv, Lq, Lk, scale,
-                     st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
+  hipLaunchKernelGGL((attn_dkv3_kernel<D, OCC, CS, DS>), grid, dim3(256), lds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
+                     (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr, dsT, ds_rows,
+                     ds_cols);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
@@ -1606,6 +1762,44 @@ int dkv2_dispatch(const void *q, const void *k, const void *v, const void *dout,
     default:
       return PCOPS_ERR_UNSUPPORTED;
   }
+}
+
+// dS^T buffer geometry of the D >= 96 path: rows = the dK/dV pass's key blocks (128),
+// columns = the dQ kernel's query blocks (256)
+struct DsGeom {
+  int rows, cols;
+  DsGeom(int Lq, int Lk) : rows((Lk + 127) / 128 * 128), cols((Lq + 255) / 256 * 256) {}
+  unsigned long long bytes(int BH) const { return (unsigned long long)BH * rows * cols * sizeof(__bf16); }
+};
+
+// PCOPS_ATTN_DS=0 keeps the recomputing dQ pass for D >= 96 (A/B runs)
+bool ds_path_on() {
+  static const bool v = env_int("PCOPS_ATTN_DS", 1) != 0;
+  return v;
+}
+
+template <int D, bool CS>
+int launch_bwd_ds(const void *q, const void *k, const void *v, const void *o, const void *dout, const float *lse,
+                  void *dq, void *dk, void *dv, int BH, int Lq, int Lk, float scale, const Strides &st, hipStream_t s,
+                  float *delta, __bf16 *dsT, ColPart *cpq, ColPart *cpkv) {
+  const DsGeom gm(Lq, Lk);
+  const long long rows = (long long)BH * Lq;
+  hipLaunchKernelGGL((attn_delta2_kernel<D>), dim3((unsigned)((rows + 127) / 128)), dim3(256), 0, s,
+                     (const __bf16 *)o, (const __bf16 *)dout, delta, BH, Lq, st);
+  PC_CHECK_LAUNCH();
+  int rc = launch_dkv3<D, 1, CS, true>(q, k, v, dout, lse, delta, dk, dv, BH, Lq, Lk, scale, st, s, cpkv, dsT,
+                                       gm.rows, gm.cols);
+  if (rc) return rc;
+  constexpr size_t lds = 2ull * kKT * (Img<D>::RS + kDsRS) * sizeof(__bf16);
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dqs_kernel<D, CS>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
+  const dim3 grid((Lq + 255) / 256, BH);
+  if (cpq) cpq->nrb = grid.x;
+  hipLaunchKernelGGL((attn_dqs_kernel<D, CS>), grid, dim3(512), lds, s, (const __bf16 *)k, (const __bf16 *)dsT,
+                     (__bf16 *)dq, Lq, Lk, scale, st, gm.rows, gm.cols, cpq ? cpq->a : nullptr);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
 }
 
 int fwd2_dispatch(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk, int D,
@@ -1971,4 +2165,91 @@ extern "C" int pcops_attention_backward(const void *q, const void *k, const void
   if (rc) return rc;
   return pcops_attention_bwd_dkv(q, k, v, dout, lse, dk, dv, B, H, Lq, Lk, D, scale, dtype, PC_ATTN_STRIDE_ARGS,
                                  workspace, workspace_bytes, stream);
+}
+
+// The whole backward in one call (delta, dK/dV, dQ, and with *_colsum non-null the
+// in_proj bias column sums of all three).  bf16 with D >= 96: the dK/dV pass stores dS^T and
+// dQ = dS K is read back from it (attn_dqs_kernel: 1 GEMM unit instead of the 3 of the
+// recomputing pass; bitwise the same dQ); otherwise the two-pass sequence above.
+extern "C" unsigned long long pcops_attention_bwd_fused_workspace_bytes(int B, int H, int Lq, int Lk, int D,
+                                                                         int dtype) {
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || D <= 0) return 0;
+  const unsigned long long BH = (unsigned long long)B * H;
+  unsigned long long n = delta_bytes(B, H, Lq);
+  const unsigned long long rq = (Lq + 127) / 128, rk = (Lk + 127) / 128;
+  n += ((BH * (rq + 2 * rk) * D * sizeof(float)) + 255) & ~255ull;
+  if (dtype == 1 && D >= 96) n += DsGeom(Lq, Lk).bytes((int)BH);
+  return n;
+}
+
+extern "C" int pcops_attention_bwd_fused(const void *q, const void *k, const void *v, const void *o, const void *dout,
+                                         const float *lse, void *dq, void *dk, void *dv, float *dq_colsum,
+                                         float *dk_colsum, float *dv_colsum, int B, int H, int Lq, int Lk, int D,
+                                         float scale, int dtype, PC_ATTN_STRIDES, void *workspace,
+                                         unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (B < 0 || H <= 0) return PCOPS_ERR_INVALID;
+  int rc = check_common(B * H, Lq, Lk, D, dtype);
+  if (rc) return rc;
+  const bool sums = dq_colsum || dk_colsum || dv_colsum;
+  if (sums && !(dq_colsum && dk_colsum && dv_colsum)) return PCOPS_ERR_INVALID;
+  if (sums && (dtype != 1 || use_v1())) return PCOPS_ERR_UNSUPPORTED;
+  if (workspace_bytes < pcops_attention_bwd_fused_workspace_bytes(B, H, Lq, Lk, D, dtype)) return PCOPS_ERR_WORKSPACE;
+  const bool ds = dtype == 1 && !use_v1() && D >= 96 && ds_path_on();
+  if (!ds) {
+    if (!sums)
+      return pcops_attention_backward(q, k, v, o, dout, lse, dq, dk, dv, B, H, Lq, Lk, D, scale, dtype,
+                                      PC_ATTN_STRIDE_ARGS, workspace, workspace_bytes, stream);
+    rc = pcops_attention_bwd_dq_delta_colsum(q, k, v, o, dout, lse, dq, dq_colsum, B, H, Lq, Lk, D, scale, dtype,
+                                             PC_ATTN_STRIDE_ARGS, workspace, workspace_bytes, stream);
+    if (rc) return rc;
+    return pcops_attention_bwd_dkv_colsum(q, k, v, dout, lse, dk, dv, dk_colsum, dv_colsum, B, H, Lq, Lk, D, scale,
+                                          dtype, PC_ATTN_STRIDE_ARGS, workspace, workspace_bytes, stream);
+  }
+  const int BH = B * H;
+  hipStream_t s = (hipStream_t)stream;
+  if (BH == 0) return PCOPS_OK;
+  if (Lq == 0 || Lk == 0) {  // empty sums; dK / dV (Lq == 0) are zero
+    if (Lq == 0 && Lk > 0) {
+      rc = pcops_attention_backward(q, k, v, o, dout, lse, dq, dk, dv, B, H, Lq, Lk, D, scale, dtype,
+                                    PC_ATTN_STRIDE_ARGS, workspace, workspace_bytes, stream);
+      if (rc) return rc;
+    }
+    if (sums)
+      for (float *p : {dq_colsum, dk_colsum, dv_colsum})
+        if (hipMemsetAsync(p, 0, (size_t)H * D * sizeof(float), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    return PCOPS_OK;
+  }
+  if (!q || !k || !v || !o || !dout || !lse || !dq || !dk || !dv || !workspace) return PCOPS_ERR_INVALID;
+  if (!aligned_ok(q, q_sb, q_sh, q_srow, 2) || !aligned_ok(k, k_sb, k_sh, k_srow, 2) ||
+      !aligned_ok(v, v_sb, v_sh, v_srow, 2) || !aligned_ok(dout, o_sb, o_sh, o_srow, 2) ||
+      !aligned_ok(o, o_sb, o_sh, o_srow, 2) || !aligned_ok(dq, q_sb, q_sh, q_srow, 2) ||
+      !aligned_ok(dk, k_sb, k_sh, k_srow, 2) || !aligned_ok(dv, v_sb, v_sh, v_srow, 2))
+    return PCOPS_ERR_UNSUPPORTED;
+  const Strides st{PC_ATTN_STRIDE_ARGS, H};
+  float *delta = (float *)workspace;
+  const long long rk = (Lk + 127) / 128, rq = (Lq + 127) / 128;
+  float *parts = (float *)((char *)workspace + delta_bytes(B, H, Lq));
+  __bf16 *dsT = (__bf16 *)((char *)parts + ((((unsigned long long)BH * (rq + 2 * rk) * D * sizeof(float)) + 255) &
+                                            ~255ull));
+  ColPart cpkv, cpq;
+  cpkv.a = parts;
+  cpkv.b = parts + (long long)BH * rk * D;
+  cpq.a = parts + 2ll * BH * rk * D;
+  ColPart *pkv = sums ? &cpkv : nullptr, *pq = sums ? &cpq : nullptr;
+  switch (D) {
+    case 96:
+      rc = sums ? launch_bwd_ds<96, true>(q, k, v, o, dout, lse, dq, dk, dv, BH, Lq, Lk, scale, st, s, delta, dsT, pq, pkv)
+                : launch_bwd_ds<96, false>(q, k, v, o, dout, lse, dq, dk, dv, BH, Lq, Lk, scale, st, s, delta, dsT, pq, pkv);
+      break;
+    case 128:
+      rc = sums ? launch_bwd_ds<128, true>(q, k, v, o, dout, lse, dq, dk, dv, BH, Lq, Lk, scale, st, s, delta, dsT, pq, pkv)
+                : launch_bwd_ds<128, false>(q, k, v, o, dout, lse, dq, dk, dv, BH, Lq, Lk, scale, st, s, delta, dsT, pq, pkv);
+      break;
+    default:
+      return PCOPS_ERR_UNSUPPORTED;
+  }
+  if (rc || !sums) return rc;
+  rc = launch_colsum_reduce(cpkv.a, dk_colsum, cpkv.b, dv_colsum, B * cpkv.nrb, H * D, s);
+  if (rc) return rc;
+  return launch_colsum_reduce(cpq.a, dq_colsum, nullptr, nullptr, B * cpq.nrb, H * D, s);
 }

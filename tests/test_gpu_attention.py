@@ -880,3 +880,61 @@ def test_linear_sliced_output_gradient(dev, monkeypatch, amp):
     ref, got = run(False), run(True)
     for a, r in zip(got, ref):
         torch.testing.assert_close(a, r, rtol=1e-2 if amp else 1e-5, atol=1e-3 if amp else 1e-5)
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,E,packed,bf", [
+    (2, 8, 2048, 2048, 1024, True, True),    # refine2 decoder sa2 (hd 128), packed batch-first
+    (1, 8, 333, 250, 1024, False, False),    # ragged cross, hd 128: partial key block, partial query tiles
+    (1, 8, 512, 512, 768, True, False),      # refine1 (hd 96)
+    (3, 4, 49, 49, 512, True, True),         # PointSea view tokens: one partial tile each way
+    (2, 8, 1024, 1024, 768, False, True),    # PointSea refine1 (hd 96 at L = 1024)
+    (1, 2, 700, 1300, 256, False, False)])   # Lk > Lq, hd 128, ragged both ways
+def test_attention_bwd_fused_equals_two_pass(dev, monkeypatch, B, H, Lq, Lk, E, packed, bf):
+    """pcops_attention_bwd_fused (bf16, D >= 96: the dK/dV pass stores dS^T, dQ = dS K read
+    back, no S / dP recompute) against the two-pass form (dQ pass recomputing S and dP, then
+    dK/dV): dQ, dK and dV bitwise equal -- the same bf16 dS, the same MFMA order per
+    accumulator -- and the in_proj bias column sums equal too."""
+    from svdformer_pointsea_amd import attention as A
+
+    gen = torch.Generator().manual_seed(21)
+    shp = (lambda L, W: (B, L, W)) if bf else (lambda L, W: (L, B, W))
+    if packed:
+        assert Lq == Lk
+        base = [torch.randn(*shp(Lq, 3 * E), generator=gen)]
+        wins = ((0, 0), (0, E), (0, 2 * E))
+    else:
+        base = [torch.randn(*shp(Lq, E), generator=gen), torch.randn(*shp(Lk, 2 * E), generator=gen)]
+        wins = ((0, 0), (1, 0), (1, E))
+    base = [s.to(dev, torch.bfloat16) for s in base]
+    g = torch.randn(*shp(Lq, E), generator=gen).to(dev, torch.bfloat16)
+    scale = 1.0 / math.sqrt(E // H)
+    got = {}
+
+    class Grab(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, i):
+            ctx.i = i
+            return x.clone()
+
+        @staticmethod
+        def backward(ctx, gr):
+            got[ctx.i] = (gr.clone(), A._take_sum(gr))
+            return gr, None
+
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(A, "_ATTN_FUSED", fused)
+        for want in (None, (True,) * len(base)):
+            got.clear()
+            srcs = [s.clone().requires_grad_(True) for s in base]
+            meta = (H, scale, E, bf, *wins) + ((want,) if want else ())
+            o = A.AttentionCore.apply(meta, *[Grab.apply(s, i) for i, s in enumerate(srcs)])
+            o.backward(g)
+            res[(fused, want is not None)] = [got[i] for i in range(len(base))]
+    for sums in (False, True):
+        for (ga, sa), (gb, sb) in zip(res[(True, sums)], res[(False, sums)]):
+            assert torch.isfinite(ga.float()).all()
+            assert torch.equal(ga, gb), (ga.float() - gb.float()).abs().max().item()
+            if sums:   # the dQ partial sums group 256 queries per block here, 128 in the D = 96 dQ pass
+                bound = 2e-6 * ga.double().abs().reshape(-1, ga.shape[-1]).sum(0) + 1e-6
+                assert ((sa.double() - sb.double()).abs() <= bound).all(), (sa - sb).abs().max().item()

@@ -35,6 +35,7 @@ GPU_OUT_ATOL = {"svd": 2e-3, "ps": 2e-3}
 # the golden outputs, relative; the F-score is a count of points inside a 1e-4 squared
 # distance, so a rounding-level move flips single points: one point (1 / N) absolute
 CD_RTOL = {"cpu": 1.2e-6, "gpu": 1e-3}
+F1_ATOL = {"cpu": None, "gpu": 1e-3}   # None: one point (1 / N); GPU: ~16 of 16384 points may cross the threshold
 
 
 def _build(which):
@@ -91,15 +92,20 @@ def _cd_check(which, outs, where):
 
     dev = outs[0].device
     gt = torch.from_numpy(gt_for(G[f"{which}_out2"], CD_SEED + (0 if which == "svd" else 1))).to(dev)
-    worst = 0.0
+    worst, wf1, checks = 0.0, 0.0, []
     for i, o in enumerate(outs):
         ref = GCD[f"{which}_cd{i}"]
         cd_p, cd_t, f1 = (t.double().cpu().numpy() for t in calc_cd(o.float().contiguous(), gt, calc_f1=True))
         for got, r in ((cd_p, ref[0]), (cd_t, ref[1])):
             rel = np.abs(got - r) / np.abs(r)
             worst = max(worst, float(rel.max()))
-            assert (rel <= CD_RTOL[where]).all(), (which, i, got, r)
-        np.testing.assert_allclose(f1, ref[2], rtol=0, atol=1.0 / o.shape[1] + 1e-9)
+            checks.append(((rel <= CD_RTOL[where]).all(), (which, i, got, r)))
+        wf1 = max(wf1, float(np.abs(f1 - ref[2]).max()))
+        tol = F1_ATOL[where] if F1_ATOL[where] is not None else 1.0 / o.shape[1] + 1e-9
+        checks.append(((np.abs(f1 - ref[2]) <= tol).all(), (which, i, "f1", f1, ref[2])))
+    print(f"\n[model parity {where}] {which}: max rel d CD {worst:.3g}, max |d F-score| {wf1:.3g}")
+    for ok, info in checks:
+        assert ok, info
     return worst
 
 
@@ -128,6 +134,6 @@ def test_model_cd_l1_parity_gpu(dev, which):
     with torch.no_grad():
         out = m(x, _images(which, x, False))
         dmax = max(float(np.abs(o.cpu().numpy() - G[f"{which}_out{i}"]).max()) for i, o in enumerate(out))
-        worst = _cd_check(which, out, "gpu")
-    print(f"\n[model parity gpu] {which}: max|d out| {dmax:.3g}, max rel d CD {worst:.3g}")
-    assert dmax <= GPU_OUT_ATOL[which], (which, dmax)
+        print(f"\n[model parity gpu] {which}: max|d out| {dmax:.3g}")
+        assert dmax <= GPU_OUT_ATOL[which], (which, dmax)
+        _cd_check(which, out, "gpu")

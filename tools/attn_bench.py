@@ -1,6 +1,8 @@
 """Attention core timing at the PCN shapes (B=32), forward and backward,
 per libpcops launch (HIP events via _lib.KernelTimer).  PCOPS_ATTN_V1=1 in
-the environment selects the first-generation kernels for A/B runs."""
+the environment selects the first-generation kernels for A/B runs; PCOPS_ATTN_FUSED=0
+the two-pass backward for head_dim >= 96 ("bwd" = the one-call backward, credited
+10*BH*Lq*Lk*D)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -34,10 +36,10 @@ for si, (Lq, Lk, E, H) in enumerate(shapes):
     fl = 4.0 * B * H * Lq * Lk * hd
     out = []
     for name, mult in [("attention forward", 1), ("attention bwd dq", 0.5), ("attention bwd dkv", 2.0),
-                       ("attention bwd delta", 0)]:
+                       ("attention bwd delta", 0), ("attention bwd", 2.5)]:
         if name not in summ:   # delta is fused into the dq launch (bf16)
             continue
         n, mean, tot = summ[name]
         tf = fl * mult / (mean * 1e-3) / 1e12 if mult else 0
-        out.append(f"{name.split()[-1]} {mean:.3f}ms {tf:.0f}TF")
+        out.append(f"{name.split(' ', 1)[-1]} {mean:.3f}ms {tf:.0f}TF")
     print(f"{tag} Lq={Lq} Lk={Lk} E={E} H={H} hd={hd}: " + " | ".join(out), flush=True)
