@@ -706,8 +706,11 @@ _GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
 # in_proj bias sums inside the attention backward passes (A/B switch)
 # the in-pass bias sums exist only in the v2/v3 bf16 kernels: the PCOPS_ATTN_V1 A/B
 # switch (libpcops returns UNSUPPORTED for *_colsum there) takes the plain passes
-# bf16, head_dim >= 96: the one-call backward with dQ from the stored dS (A/B: PCOPS_ATTN_FUSED=0)
-_ATTN_FUSED = os.environ.get("PCOPS_ATTN_FUSED", "1") != "0"
+# bf16, head_dim >= 96: the one-call backward with dQ read back from the dS the dK/dV pass
+# stores (opt-in, PCOPS_ATTN_FUSED=1): measured no faster than recomputing S / dP -- at
+# 2048^2 hd 128 the dS^T stores add 0.38 ms to the dK/dV pass and the dQ read-back takes
+# 0.57 ms, against the 0.91 ms dQ pass it replaces (profiles/r4_attn_ds_ab.txt)
+_ATTN_FUSED = os.environ.get("PCOPS_ATTN_FUSED", "0") == "1"
 _ATTN_COLSUM = (os.environ.get("PCOPS_ATTN_COLSUM", "1") != "0"
                 and os.environ.get("PCOPS_ATTN_V1", "0") != "1")
 _DEBUG_CONTIG = os.environ.get("PCOPS_DEBUG_CONTIG", "0") == "1"   # diagnostic: report _Linear operand copies

@@ -670,12 +670,7 @@ __device__ __forceinline__ void fwd2_store(__bf16 *sk, __bf16 *sv, const typenam
   }
 }
 
-// ST (guide T14, "async-stage split"): tile t+1's registers are written to LDS at the START of
-// tile t (its buffer was last read in tile t-1, before the barrier that ended it), the global
-// loads of tile t+2 are issued after tile t's QK^T, and the tile ends with the barrier alone:
-// the LDS writes overlap the QK^T MFMAs instead of sitting in front of the barrier.  The MFMA
-// sequence of every accumulator is unchanged (bitwise the same O / lse).
-template <int D, int NW, int OCC, bool ST = false>
+template <int D, int NW, int OCC>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void attn_fwd2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
                                                             const __bf16 *__restrict__ V, __bf16 *__restrict__ O,
                                                             float *__restrict__ lse, int Lq, int Lk, float scale,
@@ -703,32 +698,22 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) Y[db] = f32x16{};
   typename C::Regs kr, vr;
-  const int ntiles = (Lk + kKT - 1) / kKT;
   fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
   fwd2_store<D, NW>(sk, sv, kr, vr);
-  if constexpr (ST) {
-    if (ntiles > 1) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, kKT, Lk);
-  }
   lds_barrier();
+  const int ntiles = (Lk + kKT - 1) / kKT;
   // one tile; EDGE: the last, partial tile (key masking), compiled separately
   // so full tiles carry no per-score mask selects
   auto tile = [&](int t, auto edge_c) {
     constexpr bool EDGE = decltype(edge_c)::value;
     const int cur = t & 1;
     const int k0 = t * kKT;
-    if constexpr (ST) {
-      if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
-    } else {
-      if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
-    }
+    if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
     f32x16 X0 = f32x16{}, X1 = f32x16{};
     k_product2<D>(X0, ck, qf, X1, ck + 32 * C::kKS, qf);
     if constexpr (kSchedDs) sched_ds_mfma<D / 8, 1, 2>();
-    if constexpr (ST) {
-      if (t + 2 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + 2 * kKT, Lk);
-    }
     if constexpr (EDGE) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -762,9 +747,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
     v_product<D>(Y, cv, X0);
     v_product<D>(Y, cv + 32 * C::kVS, X1);
     if constexpr (kSchedDs) sched_ds_mfma<D / 8, 2, (OCC >= 4 ? 1 : 2)>();
-    if constexpr (!ST) {
-      if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
-    }
+    if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   };
   const int nfull = Lk / kKT;
@@ -779,27 +762,18 @@ int env_int(const char *name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-template <int D, int NW, int OCC, bool ST>
-int launch_fwd2_st(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk,
-                   float scale, const Strides &st, hipStream_t s) {
-  using C = Fwd2Cfg<D, NW>;
-  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_fwd2_kernel<D, NW, OCC, ST>,
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
-  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
-  const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
-  hipLaunchKernelGGL((attn_fwd2_kernel<D, NW, OCC, ST>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
-                     (const __bf16 *)k, (const __bf16 *)v, (__bf16 *)o, lse, Lq, Lk, scale, st);
-  PC_CHECK_LAUNCH();
-  return PCOPS_OK;
-}
-
-// PCOPS_FWD_ST: 1 = the T14 tile pipeline (stage at tile start), 0 = store at tile end (A/B)
 template <int D, int NW, int OCC>
 int launch_fwd2_occ(const void *q, const void *k, const void *v, void *o, float *lse, int BH, int Lq, int Lk,
                     float scale, const Strides &st, hipStream_t s) {
-  static const int stv = env_int("PCOPS_FWD_ST", 0);
-  return stv ? launch_fwd2_st<D, NW, OCC, true>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s)
-             : launch_fwd2_st<D, NW, OCC, false>(q, k, v, o, lse, BH, Lq, Lk, scale, st, s);
+  using C = Fwd2Cfg<D, NW>;
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_fwd2_kernel<D, NW, OCC>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
+  if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
+  const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
+  hipLaunchKernelGGL((attn_fwd2_kernel<D, NW, OCC>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (__bf16 *)o, lse, Lq, Lk, scale, st);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
 }
 
 // Occupancy: 8-wave blocks at <= 128 VGPRs run 2 blocks per CU instead of
@@ -831,7 +805,7 @@ int launch_fwd2(const void *q, const void *k, const void *v, void *o, float *lse
 // hold the two halves of the row: one permlane32 swap adds them) and written
 // to delta_out for the dK/dV pass -- no separate preprocess launch, no second
 // read of dO.
-template <int D, int NW, int OCC, bool FD, bool HS, bool CS, bool ST = false>
+template <int D, int NW, int OCC, bool FD, bool HS, bool CS>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dq2_kernel(const __bf16 *__restrict__ Q, const __bf16 *__restrict__ K,
                                                            const __bf16 *__restrict__ V, const __bf16 *__restrict__ dO,
                                                            const float *__restrict__ lse,
@@ -882,22 +856,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) Y[db] = f32x16{};
   typename C::Regs kr, vr;
-  const int ntiles = (Lk + kKT - 1) / kKT;
   fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
   fwd2_store<D, NW>(sk, sv, kr, vr);
-  if constexpr (ST) {  // attn_fwd2_kernel's ST tile pipeline
-    if (ntiles > 1) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, kKT, Lk);
-  }
   lds_barrier();
+  const int ntiles = (Lk + kKT - 1) / kKT;
   auto tile = [&](int t, auto edge_c) {
     constexpr bool EDGE = decltype(edge_c)::value;
     const int cur = t & 1;
     const int k0 = t * kKT;
-    if constexpr (ST) {
-      if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
-    } else {
-      if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
-    }
+    if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
     if constexpr (HS) {
@@ -908,9 +875,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
         f32x16 S = f32x16{}, G = f32x16{};
         k_product<D>(S, ck + 32 * hf * C::kKS, qf);
         k_product<D>(G, cv + 32 * hf * C::kVS, gf);
-        if constexpr (ST) {
-          if (hf == 0 && t + 2 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + 2 * kKT, Lk);
-        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float p = exp2_ftz(__builtin_fmaf(S[r], sl2, -lse2));
@@ -927,9 +891,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
       k_product<D>(S1, ck + 32 * C::kKS, qf);
       k_product<D>(G0, cv, gf);
       k_product<D>(G1, cv + 32 * C::kVS, gf);
-      if constexpr (ST) {
-        if (t + 2 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + 2 * kKT, Lk);
-      }
   #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float p0 = exp2_ftz(__builtin_fmaf(S0[r], sl2, -lse2));
@@ -944,9 +905,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
       v_product<D>(Y, ck, S0);
       v_product<D>(Y, ck + 32 * C::kKS, S1);
     }
-    if constexpr (!ST) {
-      if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
-    }
+    if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   };
   const int nfull = Lk / kKT;
@@ -966,7 +925,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
 // live).  MODE 1: dV only, MODE 2: dK only -- half the accumulators, so OCC = 2
 // waves per SIMD fit; the split pays one extra S recompute (5 instead of 4
 // GEMM units per key) for the second wave's latency hiding.
-template <int D, int NW, int MODE, int OCC, bool CS, bool ST = false>
+template <int D, int NW, int MODE, int OCC, bool CS>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void attn_dkv2_kernel(const __bf16 *__restrict__ Q,
                                                             const __bf16 *__restrict__ K,
                                                             const __bf16 *__restrict__ V,
@@ -1021,34 +980,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
     slse[threadIdx.x] = lr;
     sdl[threadIdx.x] = dr;
   }
-  const int ntiles = (Lq + kKT - 1) / kKT;
-  // tile t's Q / dO rows and row constants into registers
-  auto load_t = [&](int t) {
-    const int r0 = t * kKT;
-    fwd2_load<D, NW>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, r0, Lq);
-    if (threadIdx.x < kKT) {
-      const int q = r0 + threadIdx.x;
-      lr = q < Lq ? lse_b[q] * kLog2e : INFINITY;
-      dr = q < Lq ? dl_b[q] : 0.f;
-    }
-  };
-  auto store_t = [&](int slot) {
-    fwd2_store<D, NW>(sq + slot * C::kKBuf, sg + slot * C::kVBuf, qr, gr);
-    if (threadIdx.x < kKT) {
-      slse[slot * kKT + threadIdx.x] = lr;
-      sdl[slot * kKT + threadIdx.x] = dr;
-    }
-  };
-  if constexpr (ST) {  // attn_fwd2_kernel's ST tile pipeline
-    if (ntiles > 1) load_t(1);
-  }
   lds_barrier();
+  const int ntiles = (Lq + kKT - 1) / kKT;
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
-    if constexpr (ST) {
-      if (t + 1 < ntiles) store_t(cur ^ 1);
-    } else {
-      if (t + 1 < ntiles) load_t(t + 1);
+    const int r0 = t * kKT;
+    if (t + 1 < ntiles) {
+      fwd2_load<D, NW>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, r0 + kKT, Lq);
+      if (threadIdx.x < kKT) {
+        const int q = r0 + kKT + threadIdx.x;
+        lr = q < Lq ? lse_b[q] * kLog2e : INFINITY;
+        dr = q < Lq ? dl_b[q] : 0.f;
+      }
     }
     const __bf16 *cq = sq + cur * C::kKBuf;
     const __bf16 *cg = sg + cur * C::kVBuf;
@@ -1060,9 +1003,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
       k_product<D>(S1, cq + 32 * C::kKS, kf);
       k_product<D>(G0, cg, vf);  // dP (queries x keys)
       k_product<D>(G1, cg + 32 * C::kVS, vf);
-      if constexpr (ST) {
-        if (t + 2 < ntiles) load_t(t + 2);
-      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = acc_row(r, h);
@@ -1085,9 +1025,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
         f32x16 S = f32x16{}, G = f32x16{};
         k_product<D>(S, cq + 32 * hf * C::kKS, kf);
         if (MODE != 1) k_product<D>(G, cg + 32 * hf * C::kVS, vf);
-        if constexpr (ST) {
-          if (hf == 0 && t + 2 < ntiles) load_t(t + 2);
-        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = acc_row(r, h) + 32 * hf;
@@ -1099,8 +1036,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
         if (MODE != 1) v_product<D>(Y2, cq + 32 * hf * C::kKS, G);
       }
     }
-    if constexpr (!ST) {
-      if (t + 1 < ntiles) store_t(cur ^ 1);
+    if (t + 1 < ntiles) {
+      fwd2_store<D, NW>(sq + (cur ^ 1) * C::kKBuf, sg + (cur ^ 1) * C::kVBuf, qr, gr);
+      if (threadIdx.x < kKT) {
+        slse[(cur ^ 1) * kKT + threadIdx.x] = lr;
+        sdl[(cur ^ 1) * kKT + threadIdx.x] = dr;
+      }
     }
     lds_barrier();
   }
@@ -1180,6 +1121,9 @@ __device__ __forceinline__ void dkv3_rows(RowConsts &rc, const float *cl, const 
 // product): 1 = B without exp / row constants, 2 = no C MFMAs, 4 = no A MFMAs
 #ifndef PCOPS_DKV3_ABL
 #define PCOPS_DKV3_ABL 0
+#endif
+#ifndef PCOPS_DS_NT
+#define PCOPS_DS_NT 1
 #endif
 
 template <typename T>
@@ -1431,8 +1375,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
       const auto a1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
       const auto b0 = __builtin_amdgcn_permlane32_swap(w[4], w[6], false, false);
       const auto b1 = __builtin_amdgcn_permlane32_swap(w[5], w[7], false, false);
+#if PCOPS_DS_NT
+      // streaming stores: dS^T is read once, by the dQ kernel; keep the Q / dO tiles the
+      // key blocks of a head share in L2
+      __builtin_nontemporal_store((u32x4){a0[0], a1[0], a0[1], a1[1]}, reinterpret_cast<u32x4 *>(ds_row + qh0));
+      __builtin_nontemporal_store((u32x4){b0[0], b1[0], b0[1], b1[1]}, reinterpret_cast<u32x4 *>(ds_row + qh0 + 16));
+#else
       *reinterpret_cast<u32x4 *>(ds_row + qh0) = (u32x4){a0[0], a1[0], a0[1], a1[1]};
       *reinterpret_cast<u32x4 *>(ds_row + qh0 + 16) = (u32x4){b0[0], b1[0], b0[1], b1[1]};
+#endif
     }
     mid();
     Sc = Sn;
@@ -1564,7 +1515,12 @@ __global__ __launch_bounds__(512) void attn_dqs_kernel(const __bf16 *__restrict_
 #pragma unroll
     for (int c = 0; c < kDC; ++c) {
       const int idx = threadIdx.x + c * NT;
-      dr[c] = *reinterpret_cast<const bf16x8 *>(Db + (long long)(k0 + (idx >> 5)) * ds_cols + (idx & 31) * 8);
+      const bf16x8 *src = reinterpret_cast<const bf16x8 *>(Db + (long long)(k0 + (idx >> 5)) * ds_cols + (idx & 31) * 8);
+#if PCOPS_DS_NT
+      dr[c] = __builtin_nontemporal_load(src);   // read once
+#else
+      dr[c] = *src;
+#endif
     }
   };
   auto store = [&](int slot) {
@@ -1629,21 +1585,14 @@ int launch_dq2_impl(const void *q, const void *k, const void *v, const void *dou
   using C = Fwd2Cfg<D, NW>;
   constexpr int OCC = Dq2Cfg<D, NW>::kOcc;
   constexpr bool HS = Dq2Cfg<D, NW>::kHS;
-  static const bool stv = env_int("PCOPS_DQ_ST", 0) != 0;  // attn_fwd2_kernel's ST pipeline (A/B)
-  const void *fn = stv ? (const void *)attn_dq2_kernel<D, NW, OCC, FD, HS, CS, true>
-                       : (const void *)attn_dq2_kernel<D, NW, OCC, FD, HS, CS, false>;
-  static const hipError_t attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dq2_kernel<D, NW, OCC, FD, HS, CS>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::kLds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   const dim3 grid((Lq + NW * 32 - 1) / (NW * 32), BH);
   if (cp) cp->nrb = grid.x;
-  if (stv)
-    hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD, HS, CS, true>), grid, dim3(C::kThr), C::kLds, s,
-                       (const __bf16 *)q, (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta,
-                       (__bf16 *)dq, Lq, Lk, scale, st, (const __bf16 *)o, delta_out, cp ? cp->a : nullptr);
-  else
-    hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD, HS, CS, false>), grid, dim3(C::kThr), C::kLds, s,
-                       (const __bf16 *)q, (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta,
-                       (__bf16 *)dq, Lq, Lk, scale, st, (const __bf16 *)o, delta_out, cp ? cp->a : nullptr);
+  hipLaunchKernelGGL((attn_dq2_kernel<D, NW, OCC, FD, HS, CS>), grid, dim3(C::kThr), C::kLds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dq, Lq, Lk,
+                     scale, st, (const __bf16 *)o, delta_out, cp ? cp->a : nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
@@ -1766,20 +1715,13 @@ int launch_dkv2_cs(const void *q, const void *k, const void *v, const void *dout
     PC_CHECK_LAUNCH();
     return PCOPS_OK;
   }
-  static const bool stv = env_int("PCOPS_DKV_ST", 0) != 0;  // attn_fwd2_kernel's ST pipeline (A/B)
-  const void *fn = stv ? (const void *)attn_dkv2_kernel<D, NW, 0, 1, CS, true>
-                       : (const void *)attn_dkv2_kernel<D, NW, 0, 1, CS, false>;
-  static const hipError_t attr = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const hipError_t attr = hipFuncSetAttribute((const void *)attn_dkv2_kernel<D, NW, 0, 1, CS>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return PCOPS_ERR_LAUNCH;
   if (cp) cp->nrb = grid.x;
-  if (stv)
-    hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, 0, 1, CS, true>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
-                       (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
-                       (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
-  else
-    hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, 0, 1, CS, false>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
-                       (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
-                       (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
+  hipLaunchKernelGGL((attn_dkv2_kernel<D, NW, 0, 1, CS>), grid, dim3(C::kThr), lds, s, (const __bf16 *)q,
+                     (const __bf16 *)k, (const __bf16 *)v, (const __bf16 *)dout, lse, delta, (__bf16 *)dk,
+                     (__bf16 *)dv, Lq, Lk, scale, st, cp ? cp->a : nullptr, cp ? cp->b : nullptr);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
