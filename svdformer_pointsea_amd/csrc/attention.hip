@@ -1289,30 +1289,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   // they add exact zeros to dK / dV
   bf16x8 qr[kCPT], gr[kCPT];
   float lr, dr;
-  int qoff[kCPT], goff[kCPT], crow[kCPT];
-#pragma unroll
-  for (int c = 0; c < kCPT; ++c) {
-    const int idx = threadIdx.x + c * NW * 64;
-    crow[c] = idx / (D / 8);
-    qoff[c] = crow[c] * (int)st.q_srow + (idx % (D / 8)) * 8;
-    goff[c] = crow[c] * (int)st.o_srow + (idx % (D / 8)) * 8;
-  }
+  // The per-thread tile offsets are recomputed at every use from an opaque copy of
+  // threadIdx.x (a few integer ops): hoisted out of the tile loop they are ~20 loop-
+  // invariant VGPRs, which the 512-register one-wave-per-SIMD body cannot hold -- the
+  // *_colsum build spilled them and reloaded ~50 dwords from scratch per tile, each
+  // reload a vector-memory op queued (vmcnt, in order) behind the tile loads.
+  auto tid_ = [] {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+  };
   auto load = [&](int t) {
     const int r0 = t * kKT;
     if (r0 + kKT <= Lq) {
       const __bf16 *qb = Qb + (long long)r0 * st.q_srow, *gb = Gb + (long long)r0 * st.o_srow;
+      const int tid = tid_();
 #pragma unroll
       for (int c = 0; c < kCPT; ++c) {
-        qr[c] = *reinterpret_cast<const bf16x8 *>(qb + qoff[c]);
-        gr[c] = *reinterpret_cast<const bf16x8 *>(gb + goff[c]);
+        const int idx = tid + c * NW * 64;
+        const int row = idx / (D / 8), col = (idx % (D / 8)) * 8;
+        qr[c] = *reinterpret_cast<const bf16x8 *>(qb + row * (int)st.q_srow + col);
+        gr[c] = *reinterpret_cast<const bf16x8 *>(gb + row * (int)st.o_srow + col);
       }
       lr = lse_b[r0 + l] * kLog2e;
       dr = dl_b[r0 + l];
     } else {
+      const int tid = tid_();
 #pragma unroll
       for (int c = 0; c < kCPT; ++c) {
-        const int idx = threadIdx.x + c * NW * 64;
-        const long long rr = min(r0 + crow[c], Lq - 1);
+        const int idx = tid + c * NW * 64;
+        const long long rr = min(r0 + idx / (D / 8), Lq - 1);
         qr[c] = *reinterpret_cast<const bf16x8 *>(Qb + rr * st.q_srow + (idx % (D / 8)) * 8);
         gr[c] = *reinterpret_cast<const bf16x8 *>(Gb + rr * st.o_srow + (idx % (D / 8)) * 8);
       }
@@ -1325,9 +1331,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   };
   // every wave writes the same 64 lse / delta values (no wave-dependent branch)
   auto store = [&](int slot) {
+    const int tid = tid_();
 #pragma unroll
     for (int c = 0; c < kCPT; ++c) {
-      const int idx = threadIdx.x + c * NW * 64;
+      const int idx = tid + c * NW * 64;
       const int row = idx / (D / 8), ch = idx % (D / 8);
       *reinterpret_cast<bf16x8 *>(sq + slot * TB + img_off<D>(row, ch)) = qr[c];
       *reinterpret_cast<bf16x8 *>(sg + slot * TB + img_off<D>(row, ch)) = gr[c];
