@@ -259,6 +259,14 @@ int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, 
  * that feeds only GEMMs, models/model_utils.py:616).  16-byte aligned operands. */
 int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype, long long n,
               pcops_stream_t stream);
+/* pcops_add_posemb: out[b][m][h] = a[b][m][h] + E[b][h*N + m] for (B, N, H) token-major a / out,
+ * where E (B, N*H) is SinusoidalPositionalEmbedding(cd) (models/model_utils.py:883-917:
+ * E[b][n*H + 2i] = sin(cd[b][n] * div_term[i]), E[b][n*H + 2i + 1] = cos(...)) read through SDG's
+ * raw .reshape(B, hidden, N).permute (SVDFormer.py:77-80, PointSea SDG the same): the query /
+ * key input `with_pos_embed(src1, pos)` of the SDG's first self_attention, summed in fp32 and
+ * stored once as out_dtype.  H % 8 == 0, 16-byte aligned a / out. */
+int pcops_add_posemb(const void *a, int a_dtype, const float *cd, const float *div_term, int B, int N, int H,
+                     void *out, int out_dtype, pcops_stream_t stream);
 /* pcops_layernorm_fwd: x = a (+ b); y = (x - mean) * rstd * gamma + beta per row
  * (torch.nn.LayerNorm over the last dim), written as fp32 (y32) and/or bf16
  * (y16); mean / rstd (rows) saved for the backward.  C <= 1024, C % 8 == 0,

@@ -58,6 +58,7 @@ _SIGS = {
     "pcops_attention_bwd_dkv_colsum": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, LL, P, ULL, P]),
     "pcops_transpose_add": (I, [P, I, P, I, P, I, P, I, I, I, I, P]),
     "pcops_add": (I, [P, I, P, I, P, I, LL, P]),
+    "pcops_add_posemb": (I, [P, I, P, P, I, I, I, P, I, P]),
     "pcops_edge_group": (I, [P, P, I, I, I, I, P, I, P]),
     "pcops_edge_group_grad": (I, [P, I, P, I, I, I, I, P, P]),
     "pcops_max_k": (I, [P, I, LL, I, I, P, P, P]),

@@ -683,15 +683,59 @@ class _AddToBf16(Function):
         return ga, (ga if ctx.dts[1] == ctx.dts[0] else g.to(ctx.dts[1]))
 
 
+class PosEmbedding:
+    """SDG's positional term, kept lazy: SinusoidalPositionalEmbedding(cd) (models/model_utils.py:
+    883-917) read through the reference's raw .reshape(B, hidden, N).permute (SVDFormer.py:77-80),
+    token-major (B, N, hidden).  Its only consumer is `with_pos_embed(src1, pos)` feeding the q / k
+    projection; block_sum adds it there in one kernel (pcops_add_posemb) instead of materialising
+    sin, cos, the interleave and the transposed copy.  `tensor()` is the plain torch expression."""
+
+    def __init__(self, cd, embedding, hidden):
+        self.cd = cd.float().contiguous()            # (B, N) half Chamfer distances / sigma
+        self.embedding, self.hidden = embedding, hidden
+
+    def tensor(self):
+        B, N = self.cd.shape
+        return self.embedding(self.cd).reshape(B, self.hidden, N).transpose(1, 2)
+
+
+class _AddPosBf16(Function):
+    """bf16(s + pos) with pos = PosEmbedding computed in the kernel (no gradient: the reference
+    .detach()es the embedding); backward: the gradient of s, cast once like _AddToBf16."""
+
+    @staticmethod
+    def forward(ctx, s, cd, div):
+        B, N, H = s.shape
+        s = s.contiguous()
+        out = torch.empty(s.shape, dtype=torch.bfloat16, device=s.device)
+        with torch.cuda.device(s.device):
+            call("add_posemb", lib().pcops_add_posemb, ptr(s), _dt(s), ptr(cd), ptr(div), B, N, H, ptr(out), 1,
+                 stream_of(s))
+        ctx.sdt = s.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.sdt), None, None
+
+
 def block_sum(s, f):
     """s + f of a block's (residual, FFN) outputs whose consumers are GEMMs
-    (input_proj / conv_ps): bf16 directly under bf16 autocast, else s + f."""
+    (input_proj / conv_ps): bf16 directly under bf16 autocast, else s + f.
+    f may be a PosEmbedding (the SDG query's positional term)."""
+    if isinstance(f, PosEmbedding):
+        if (_PCOPS_POSEMB and _want_bf16() and s.is_cuda and s.dim() == 3 and s.shape[-1] % 8 == 0
+                and s.dtype in _DT):
+            div = f.embedding.div_term.float().contiguous()
+            return _AddPosBf16.apply(s, f.cd, div)
+        f = f.tensor()
     if _BLOCK_SUM16 and _want_bf16() and s.is_cuda:
         return _AddToBf16.apply(s, f)
     return s + f
 
 
 _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
+_PCOPS_POSEMB = os.environ.get("PCOPS_POSEMB", "1") != "0"          # A/B switch: fused add + positional embedding
 _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
 _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
 _WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switch: split-K weight gradients

@@ -397,6 +397,39 @@ void add_go(const void *a, const void *b, void *out, long long n8, hipStream_t s
   hipLaunchKernelGGL((add_kernel<AT, BT, OT>), dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, s, a, b, out, n8);
 }
 
+// ---------------------------------------------------------------- add + positional embedding
+// out[b][m][h] = a[b][m][h] + E[b][h*N + m], E = SinusoidalPositionalEmbedding(cd) flattened per
+// batch: E[b][n*H + 2i + c] = (c ? cos : sin)(cd[b][n] * div[i])  (models/model_utils.py:883-917,
+// with SDG's raw .reshape(B, hidden, N).permute of it, SVDFormer.py:77-80) -- the sum computed in
+// fp32 and stored once in out's dtype, as autocast does before the q / k projection GEMM.
+// Replaces torch's sin, cos, mul, cat, the transposed view's copy and the add (7 launches, ~1.4 GB
+// per SDG stage at PCN shapes) by one pass over a.
+template <int AT, int OT>
+__global__ __launch_bounds__(256) void add_posemb_kernel(const void *__restrict__ a, const float *__restrict__ cd,
+                                                         const float *__restrict__ div, int N, int H,
+                                                         void *__restrict__ out, long long n8) {
+  const int H8 = H >> 3;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    V8 x;
+    ld8c<AT>(x, a, 8 * i);
+    const long long row = i / H8;            // b * N + m
+    const int h0 = (int)(i - row * H8) * 8;
+    const int b = (int)(row / N), m = (int)(row - (long long)b * N);
+    const float *cdb = cd + (long long)b * N;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const long long f = (long long)(h0 + k) * N + m;
+      const int n = (int)(f / H), j = (int)(f - (long long)n * H);
+      const float w = cdb[n] * div[j >> 1];
+      x.v[k] += (j & 1) ? cosf(w) : sinf(w);
+    }
+    if constexpr (OT == 0)
+      st8_f32(reinterpret_cast<float *>(out), 8 * i, x);
+    else
+      st8_bf16(reinterpret_cast<__bf16 *>(out), 8 * i, x);
+  }
+}
+
 // ---------------------------------------------------------------- column sum
 // out[c] = sum_r g[r][c]: the bias gradient of the blocks' Linear / 1x1-conv
 // layers (torch's bf16 sum(0) runs at 0.8-3 TB/s on these (65536, C) inputs).
@@ -784,6 +817,25 @@ void colsum_shape(long long rows, int C, int &chunks, long long &rpc) {
 }
 
 }  // namespace
+
+extern "C" int pcops_add_posemb(const void *a, int a_dtype, const float *cd, const float *div_term, int B, int N,
+                                int H, void *out, int out_dtype, pcops_stream_t stream) {
+  if (B < 0 || N < 0 || H <= 0 || (H & 7) || !dt_ok(a_dtype) || !dt_ok(out_dtype)) return PCOPS_ERR_INVALID;
+  if (B == 0 || N == 0) return PCOPS_OK;
+  if (!a || !cd || !div_term || !out) return PCOPS_ERR_INVALID;
+  const long long n8 = (long long)B * N * H / 8;
+  long long g = (n8 + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipStream_t s = (hipStream_t)stream;
+  switch (a_dtype * 2 + out_dtype) {
+    case 0: hipLaunchKernelGGL((add_posemb_kernel<0, 0>), dim3((unsigned)g), dim3(256), 0, s, a, cd, div_term, N, H, out, n8); break;
+    case 1: hipLaunchKernelGGL((add_posemb_kernel<0, 1>), dim3((unsigned)g), dim3(256), 0, s, a, cd, div_term, N, H, out, n8); break;
+    case 2: hipLaunchKernelGGL((add_posemb_kernel<1, 0>), dim3((unsigned)g), dim3(256), 0, s, a, cd, div_term, N, H, out, n8); break;
+    default: hipLaunchKernelGGL((add_posemb_kernel<1, 1>), dim3((unsigned)g), dim3(256), 0, s, a, cd, div_term, N, H, out, n8); break;
+  }
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
 
 extern "C" int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype,
                          long long n, pcops_stream_t stream) {

@@ -27,7 +27,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import SDG_Decoder_PointSea, cross_attention, self_attention, to_tokens
+from .attention import PosEmbedding, SDG_Decoder_PointSea, cross_attention, self_attention, to_tokens
 from .chamfer3D import chamfer_3DDist
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act
@@ -114,7 +114,7 @@ class SDG(nn.Module):
         Fx = torch.cat([Fx, g.expand(B, N, g.shape[-1]).to(Fx.dtype)], dim=-1)
         # structure analysis (PointSea.py:100-105): half Chamfer to the partial input
         half_cd = self.cd_distance(coarse.float().contiguous(), partial.float().contiguous())[0] / self.sigma_d
-        pos = self.embedding(half_cd).reshape(B, self.hidden, N).transpose(1, 2)
+        pos = PosEmbedding(half_cd, self.embedding, self.hidden)   # added inside the q / k input
         s, f = self.sa1.forward_tokens(Fx, pos)
         F_Q = s + f
         F_Q_ = self.decoder1.forward_tokens(F_Q)           # PointSea's decoder ignores pos

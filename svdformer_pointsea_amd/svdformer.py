@@ -19,7 +19,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import SDG_Decoder, block_sum, cross_attention, linear, self_attention, to_channels, to_tokens
+from .attention import (PosEmbedding, SDG_Decoder, block_sum, cross_attention, linear, self_attention, to_channels,
+                        to_tokens)
 from .chamfer3D import chamfer_3DDist
 from .model_utils import edge_features, fps_subsample, group_local, sample_and_group_knn, sample_and_group_knn_cl
 from ._lib import fork
@@ -482,7 +483,7 @@ class SDG(nn.Module):
         # structure analysis: half Chamfer distance to the partial input
         half_cd = self.cd_distance(coarse.float().contiguous(), partial.float().contiguous())[0] / self.sigma
         # (B,N,hidden).reshape(B,hidden,N).permute(2,0,1) of the reference, token-major
-        pos = self.embedding(half_cd).reshape(B, self.hidden, N).transpose(1, 2)
+        pos = PosEmbedding(half_cd, self.embedding, self.hidden)   # added inside the q / k input
         s, f = self.sa1.forward_tokens(F_, pos)
         F_Q = block_sum(s, f)   # feeds decoder1 / cross1, both starting with input_proj
         F_Q_ = self._decode(self.decoder1, F_Q)

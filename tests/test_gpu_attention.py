@@ -938,3 +938,31 @@ def test_attention_bwd_fused_equals_two_pass(dev, monkeypatch, B, H, Lq, Lk, E, 
             if sums:   # the dQ partial sums group 256 queries per block here, 128 in the D = 96 dQ pass
                 bound = 2e-6 * ga.double().abs().reshape(-1, ga.shape[-1]).sum(0) + 1e-6
                 assert ((sa.double() - sb.double()).abs() <= bound).all(), (sa - sb).abs().max().item()
+
+
+@pytest.mark.parametrize("B,N,H,sdt", [(2, 2048, 512, torch.float32), (3, 512, 768, torch.float32),
+                                       (2, 1024, 256, torch.bfloat16), (1, 100, 64, torch.float32)])
+def test_add_posemb_kernel(dev, B, N, H, sdt):
+    """pcops_add_posemb (block_sum of an SDG query and its PosEmbedding under bf16 autocast)
+    against the torch expression it replaces -- SinusoidalPositionalEmbedding, the raw
+    .reshape(B, hidden, N).transpose, the fp32 add, one bf16 rounding: equal up to one bf16
+    ulp where sinf / cosf differ in the last fp32 bit; gradient = the cast upstream gradient."""
+    from svdformer_pointsea_amd.attention import PosEmbedding, block_sum
+    from svdformer_pointsea_amd.svdformer import SinusoidalPositionalEmbedding
+
+    gen = torch.Generator().manual_seed(B * N + H)
+    emb = SinusoidalPositionalEmbedding(H).to(dev)
+    cd = (torch.rand(B, N, generator=gen) * 40).to(dev)     # half_cd / sigma: O(10)
+    s = torch.randn(B, N, H, generator=gen).to(dev, sdt).requires_grad_(True)
+    pos = PosEmbedding(cd, emb, H)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        got = block_sum(s, pos)
+    ref = (s.detach().float() + pos.tensor()).to(torch.bfloat16)
+    assert got.dtype == torch.bfloat16 and got.shape == (B, N, H)
+    diff = (got.float() - ref.float()).abs()
+    ulp = ref.float().abs().clamp_min(1e-30) * 2.0 ** -7
+    assert (diff <= ulp).all(), diff.max().item()
+    assert (got == ref).float().mean().item() > 0.999
+    g = torch.randn(B, N, H, generator=gen).to(dev, torch.bfloat16)
+    got.backward(g)
+    assert s.grad.dtype == sdt and torch.equal(s.grad, g.to(sdt))

@@ -1,10 +1,8 @@
 set -o pipefail
-O=gpurun_out/r4h; mkdir -p $O
-export PYTEST_K="core_bf16 or attention_bwd_colsum or fused_equals or core_backward_fp32"
-bash tools/gpu_run.sh $O tests_k || exit 1
-for i in 1 2; do
-  ATTN_BENCH_SUMS=1 timeout -k 10 300 python tools/attn_bench.py 0 1 3 > $O/sums_new_$i.txt 2>&1 || exit 1
-  ATTN_BENCH_SUMS=1 PCOPS_LIB_PATH=$PWD/tools/ab/libpcops_prev.so timeout -k 10 300 python tools/attn_bench.py 0 1 3 > $O/sums_prev_$i.txt 2>&1 || exit 1
-done
-timeout -k 10 400 python tools/glue_ops.py > $O/glue_ops.txt 2>&1 || exit 1
-bash tools/gpu_run.sh $O trace_fp32 trace_c1
+O=gpurun_out/r4j; mkdir -p $O
+cp tuning/tunableop_svdformer_gfx950.csv $O/tunableop_svdformer_gfx950.prev.csv
+timeout -k 10 900 python bench.py --tunableop tune --steps 2 --warmup 1 --no-cpu-baseline --no-extra-legs --no-kernel-timing --no-fp32-leg > $O/tune.json 2> $O/tune.err || exit 1
+cp tuning/tunableop_svdformer_gfx950.csv $O/tunableop_svdformer_gfx950.csv
+timeout -k 10 400 python bench.py --no-cpu-baseline --no-extra-legs --no-fp32-leg > $O/bench_newtune.json 2> $O/bench_newtune.err || exit 1
+cp $O/tunableop_svdformer_gfx950.prev.csv tuning/tunableop_svdformer_gfx950.csv
+timeout -k 10 400 python bench.py --no-cpu-baseline --no-extra-legs --no-fp32-leg > $O/bench_oldtune.json 2> $O/bench_oldtune.err
