@@ -131,6 +131,13 @@ int pcops_three_interpolate_grad(const float *grad_out, const int *idx, const fl
  * idx (B,S,K) int32; dist (B,S,K) optional (may be NULL).  C <= 512, K+pad <= 64. */
 int pcops_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
               pcops_stream_t stream);
+/* The same with scratch (pcops_knn_workspace_bytes; 0 = none needed): for C == 3, K + pad <= 16,
+ * S and N <= 4096 both clouds are sorted by Morton code first and each block of 64 spatially
+ * adjacent queries scans the candidates nearest-first -- the same output bit for bit (every
+ * candidate is still compared, as a (distance, index) pair); otherwise pcops_knn. */
+unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int C, int K);
+int pcops_knn_ws(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
+                 void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 
 /* ---------------- Chamfer (metrics/CD/chamfer3D) ----------------
  * chamfer_3D.forward(xyz1, xyz2, dist1, dist2, idx1, idx2): chamfer_cuda.cpp:17-33,

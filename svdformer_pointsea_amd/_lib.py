@@ -39,6 +39,8 @@ _SIGS = {
     "pcops_three_interpolate": (I, [P, P, P, I, I, I, I, P, P]),
     "pcops_three_interpolate_grad": (I, [P, P, P, I, I, I, I, P, P]),
     "pcops_knn": (I, [P, P, I, I, I, I, I, I, P, P, P]),
+    "pcops_knn_workspace_bytes": (ULL, [I, I, I, I, I]),
+    "pcops_knn_ws": (I, [P, P, I, I, I, I, I, I, P, P, P, ULL, P]),
     "pcops_chamfer_forward": (I, [P, P, I, I, I, P, P, P, P, P]),
     "pcops_chamfer_backward": (I, [P, P, I, I, I, P, P, P, P, P, P, P]),
     "pcops_emd_workspace_bytes": (ULL, [I, I]),

@@ -15,10 +15,12 @@ its model classes can import them unchanged:
   PCViews                                               :1179-1234
 """
 import numpy as np
+import os
+
 import torch
 from torch import nn
 
-from ._lib import call, lib, ptr, require_float, stream_of
+from ._lib import Workspace, call, lib, ptr, require_float, stream_of
 from .pointnet2_utils import furthest_point_sample, gather_operation, grouping_operation
 
 
@@ -37,8 +39,17 @@ def _knn(q, p, k, pad=0, want_dist=False):
     idx = torch.empty(B, S, k, dtype=torch.int32, device=q.device)
     dist = torch.empty(B, S, k, dtype=torch.float32, device=q.device) if want_dist else None
     with torch.cuda.device(q.device):
-        call("knn", lib().pcops_knn, ptr(q), ptr(p), B, S, N, C, k, pad, ptr(idx), ptr(dist), stream_of(q))
+        wsb = lib().pcops_knn_workspace_bytes(B, S, N, C, k + pad) if _KNN_SORTED else 0
+        if wsb:   # C == 3: the Morton-ordered scan (knn.hip knn3s_kernel), same result bit for bit
+            ws = Workspace.get(q.device, wsb)
+            call("knn", lib().pcops_knn_ws, ptr(q), ptr(p), B, S, N, C, k, pad, ptr(idx), ptr(dist), ptr(ws), wsb,
+                 stream_of(q))
+        else:
+            call("knn", lib().pcops_knn, ptr(q), ptr(p), B, S, N, C, k, pad, ptr(idx), ptr(dist), stream_of(q))
     return (idx, dist) if want_dist else idx
+
+
+_KNN_SORTED = os.environ.get("PCOPS_KNN_SORTED", "1") != "0"   # A/B switch
 
 
 def query_knn(nsample, xyz, new_xyz, include_self=True):
