@@ -655,6 +655,194 @@ __global__ __launch_bounds__(64 * G) void knn3s_kernel(const float4 *__restrict_
 }
 
 // candidates (float4, index, code), then the queries' (S == 0: self kNN, shared)
+// ----------------------------------------------------------------- C >= 32, streamed (v3)
+// knnC2_kernel's arithmetic (4x4 register micro-tile, each distance a sequential fma chain over
+// the channels in order, then ((-2 dot) + |q|^2) + |p|^2 with torch_sumsq norms) with the
+// latency it exposed removed: at the model's shapes (S, N <= 1024, C = 64 / 256) its grid was
+// 256 blocks of 4 waves (one wave per SIMD) whose every 32-channel chunk was staged by scalar
+// loads between two barriers, and each candidate tile recomputed |p|^2 serially from global
+// memory.  Here the norms come from a separate pass (knn_norms_kernel), the (query chunk,
+// candidate chunk) stream is double-buffered through registers (float4 loads of step k+1 issue
+// before step k's fmas, one barrier per step), and the candidate range is split over `splits`
+// blocks whose sorted partial lists knn_merge_kernel merges as (distance, index) pairs.
+__global__ __launch_bounds__(256) void knn_norms_kernel(const float *__restrict__ x, long long rows, int C,
+                                                        float *__restrict__ out) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r < rows) out[r] = torch_sumsq(x + r * C, C);
+}
+
+template <int KK>
+__global__ __launch_bounds__(256) void knnC3_kernel(const float *__restrict__ q, const float *__restrict__ p,
+                                                    const float *__restrict__ qnorm, const float *__restrict__ pnorm,
+                                                    int S, int N, int C, int splits, int span, int K, int pad,
+                                                    int *__restrict__ idx, float *__restrict__ dist,
+                                                    float *__restrict__ part_d, int *__restrict__ part_i) {
+  constexpr int QT = 64, CT = 64, CC = 32, LS = CC + 4, SLOT = QT * LS;
+  constexpr int CAP = 8, NT = 256;
+  // one LDS arena: the two chunk slots of each side; at a tile's end the distance tile over
+  // the query slots (between barriers); at the end the wave merge over all of it
+  constexpr size_t kArena = sizeof(MergeBuf<KK, 4>) > 4 * SLOT * sizeof(float) ? sizeof(MergeBuf<KK, 4>)
+                                                                                   : 4 * SLOT * sizeof(float);
+  static_assert(QT * (CT + 1) <= 2 * SLOT, "distance tile must fit the query slots");
+  __shared__ __attribute__((aligned(16))) unsigned char arena[kArena];
+  __shared__ int2 queue_[CAP * NT];
+  float *sq = reinterpret_cast<float *>(arena);
+  float *sp = sq + 2 * SLOT;
+  float(*sd)[CT + 1] = reinterpret_cast<float(*)[CT + 1]>(arena);
+  struct {
+    int2 *queue;
+    MergeBuf<KK, 4> &mb;
+  } sh{queue_, *reinterpret_cast<MergeBuf<KK, 4> *>(arena)};
+  const int b = blockIdx.y, t = threadIdx.x, tq = t >> 4, tc = t & 15;
+  const int w = t >> 6, lane = t & 63;
+  const int qt = blockIdx.x / splits, sp_i = blockIdx.x - qt * splits;
+  const int q0 = qt * QT;
+  const int n0 = sp_i * span, n1 = min(N, n0 + span);
+  const float *qb = q + (size_t)b * S * C;
+  const float *pb = p + (size_t)b * N * C;
+  const int s = q0 + lane;
+  const int sc = s < S ? s : S - 1;
+  TopK<KK, CAP, NT> tk;
+  tk.init();
+  const int nch = (C + CC - 1) / CC, ntile = (n1 - n0 + CT - 1) / CT, steps = nch * ntile;
+  // this thread's two float4 of each side per step: rows r = e / 8 (e = t, t + 256), channels 4 (e % 8)
+  float4 rq[2], rp[2];
+  auto load = [&](int k) {
+    const int tile = k / nch, ch = k - tile * nch;
+    const int t0 = n0 + tile * CT, c0 = ch * CC, cw = min(CC, C - c0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = t + 256 * u, r = e >> 3, c = (e & 7) * 4;
+      const int qi = q0 + r, pi = t0 + r;
+      if (cw == CC) {
+        rq[u] = qi < S ? *reinterpret_cast<const float4 *>(qb + (size_t)qi * C + c0 + c) : make_float4(0, 0, 0, 0);
+        rp[u] = pi < n1 ? *reinterpret_cast<const float4 *>(pb + (size_t)pi * C + c0 + c) : make_float4(0, 0, 0, 0);
+      } else {
+        float a[4], z[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a[i] = (qi < S && c + i < cw) ? qb[(size_t)qi * C + c0 + c + i] : 0.f;
+          z[i] = (pi < n1 && c + i < cw) ? pb[(size_t)pi * C + c0 + c + i] : 0.f;
+        }
+        rq[u] = make_float4(a[0], a[1], a[2], a[3]);
+        rp[u] = make_float4(z[0], z[1], z[2], z[3]);
+      }
+    }
+  };
+  float acc[4][4];
+  if (steps > 0) load(0);
+  for (int k = 0; k < steps; ++k) {
+    const int slot = k & 1, tile = k / nch, ch = k - tile * nch;
+    const int t0 = n0 + tile * CT, cw = min(CC, C - ch * CC);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = t + 256 * u, r = e >> 3, c = (e & 7) * 4;
+      *reinterpret_cast<float4 *>(sq + slot * SLOT + r * LS + c) = rq[u];
+      *reinterpret_cast<float4 *>(sp + slot * SLOT + r * LS + c) = rp[u];
+    }
+    __syncthreads();
+    if (k + 1 < steps) load(k + 1);
+    if (ch == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    }
+    const float *cq = sq + slot * SLOT, *cp = sp + slot * SLOT;
+    int c = 0;
+    for (; c + 4 <= cw; c += 4) {
+      float4 qv[4], pv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qv[i] = *reinterpret_cast<const float4 *>(cq + (tq + 16 * i) * LS + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pv[j] = *reinterpret_cast<const float4 *>(cp + (tc + 16 * j) * LS + c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = __builtin_fmaf(qv[i].x, pv[j].x, acc[i][j]);
+          acc[i][j] = __builtin_fmaf(qv[i].y, pv[j].y, acc[i][j]);
+          acc[i][j] = __builtin_fmaf(qv[i].z, pv[j].z, acc[i][j]);
+          acc[i][j] = __builtin_fmaf(qv[i].w, pv[j].w, acc[i][j]);
+        }
+    }
+    for (; c < cw; ++c) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_fmaf(cq[(tq + 16 * i) * LS + c], cp[(tc + 16 * j) * LS + c], acc[i][j]);
+    }
+    if (ch == nch - 1) {  // the tile's distances, then its selection
+      __syncthreads();    // every thread is past its reads of the query slots
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = min(q0 + tq + 16 * i, S - 1);
+        const float qn = qnorm[(size_t)b * S + qr];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pr = min(t0 + tc + 16 * j, N - 1);
+          sd[tq + 16 * i][tc + 16 * j] = ((-2.f * acc[i][j]) + qn) + pnorm[(size_t)b * N + pr];
+        }
+      }
+      __syncthreads();
+      const int e1 = min(CT, n1 - t0);
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int e = w * 16 + kk;
+        if (e < e1) tk.offer(sh.queue, t, sd[lane][e], t0 + e);
+        if (kk == 7 || kk == 15) tk.maybe_drain(sh.queue, t, 8);
+      }
+      __syncthreads();    // the distance tile is read before the next step's query chunk lands
+    }
+  }
+  tk.drain(sh.queue, t);
+  if (splits == 1) {
+    merge_and_store<KK, 4>(sh.mb, tk.bd, tk.bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
+                           dist ? dist + ((size_t)b * S + sc) * K : nullptr);
+    return;
+  }
+  // the block's sorted top-KK over its candidate range (all KK entries, no pad), for the merge
+  const size_t row = (((size_t)b * S + sc) * splits + sp_i) * KK;
+  merge_and_store<KK, 4>(sh.mb, tk.bd, tk.bi, w, lane, s < S, KK, 0, n1 - n0 < KK ? n1 - n0 : KK, part_i + row,
+                         part_d + row);
+}
+
+// per query: the splits' sorted (distance, index) lists merged lexicographically (the index-order
+// scan's result: every list is the exact top-KK of its range), entries [pad, pad + K) stored
+template <int KK>
+__global__ __launch_bounds__(256) void knn_merge_kernel(const float *__restrict__ part_d, const int *__restrict__ part_i,
+                                                        long long rows, int splits, int span, int N, int K, int pad,
+                                                        int *__restrict__ idx, float *__restrict__ dist) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  int head[16];
+  for (int g = 0; g < splits; ++g) head[g] = 0;
+  for (int o = 0; o < K + pad; ++o) {
+    float bdv = INFINITY;
+    int biv = INT_MAX, bw = -1;
+    for (int g = 0; g < splits; ++g) {
+      const int avail = min(KK, min(N, (g + 1) * span) - g * span);
+      if (head[g] < avail) {
+        const size_t e = (r * splits + g) * KK + head[g];
+        const float dv = part_d[e];
+        const int iv = part_i[e];
+        if (bw < 0 || dv < bdv || (dv == bdv && iv < biv)) {
+          bdv = dv;
+          biv = iv;
+          bw = g;
+        }
+      }
+    }
+    if (bw >= 0) head[bw] += 1;
+    if (o >= pad) {
+      const bool ok = o < N && bw >= 0;
+      idx[r * K + o - pad] = ok ? biv : 0;
+      if (dist) dist[r * K + o - pad] = ok ? bdv : 0.f;
+    }
+  }
+}
+
 size_t knn_sorted_bytes(int B, int S, int N) {
   auto a = [](size_t x) { return (x + 255) & ~size_t(255); };
   auto part = [&](int n) { return a((size_t)B * n * 16) + 2 * a((size_t)B * n * 4); };
@@ -753,9 +941,55 @@ int launch_knn(const float *q, const float *p, int B, int S, int N, int C, int K
 
 }  // namespace
 
+// feature-space kNN scratch: both clouds' norms, then the splits' partial lists
+int kk_of(int kk) { return kk <= 4 ? 4 : kk <= 8 ? 8 : kk <= 16 ? 16 : kk <= 20 ? 20 : 32; }
+int knnC3_splits(int B, int S, int N) {
+  const int blocks = (S + 63) / 64 * B;
+  int sp = (1024 + blocks - 1) / blocks;
+  sp = sp < 1 ? 1 : (sp > 16 ? 16 : sp);
+  while (sp > 1 && (N + sp - 1) / sp < 64) --sp;
+  return sp;
+}
+size_t knnC3_bytes(int B, int S, int N, int kk) {
+  auto a = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t parts = (size_t)B * S * knnC3_splits(B, S, N) * kk_of(kk);
+  return a((size_t)B * S * 4) + a((size_t)B * N * 4) + 2 * a(parts * 4);
+}
+
+template <int KK>
+int launch_knnC3(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
+                 void *ws, hipStream_t st) {
+  auto a = [](size_t x) { return (x + 255) & ~size_t(255); };
+  char *w = (char *)ws;
+  float *qn = (float *)w;
+  w += a((size_t)B * S * 4);
+  float *pn = (float *)w;
+  w += a((size_t)B * N * 4);
+  const int splits = knnC3_splits(B, S, N);
+  const size_t parts = (size_t)B * S * splits * KK;
+  float *pd = (float *)w;
+  w += a(parts * 4);
+  int *pi = (int *)w;
+  const long long rq = (long long)B * S, rp = (long long)B * N;
+  const bool self = q == p && S == N;
+  hipLaunchKernelGGL(knn_norms_kernel, dim3((unsigned)((rp + 255) / 256)), dim3(256), 0, st, p, rp, C, pn);
+  if (!self) hipLaunchKernelGGL(knn_norms_kernel, dim3((unsigned)((rq + 255) / 256)), dim3(256), 0, st, q, rq, C, qn);
+  const int span = ((N + splits - 1) / splits + 63) / 64 * 64;
+  const dim3 grid((S + 63) / 64 * splits, B);
+  hipLaunchKernelGGL((knnC3_kernel<KK>), grid, dim3(256), 0, st, q, p, self ? pn : qn, pn, S, N, C, splits, span, K,
+                     pad, idx, dist, pd, pi);
+  if (splits > 1)
+    hipLaunchKernelGGL((knn_merge_kernel<KK>), dim3((unsigned)((rq + 255) / 256)), dim3(256), 0, st, pd, pi, rq,
+                       splits, span, N, K, pad, idx, dist);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
 extern "C" unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int C, int K) {
-  if (B <= 0 || S <= 0 || N <= 0 || C != 3 || K <= 0) return 0;
-  return knn_sorted_bytes(B, S, N);
+  if (B <= 0 || S <= 0 || N <= 0 || C <= 0 || K <= 0) return 0;
+  if (C == 3) return knn_sorted_bytes(B, S, N);
+  if (C >= 32 && C <= 512 && K <= 32) return knnC3_bytes(B, S, N, K);
+  return 0;
 }
 
 extern "C" int pcops_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx,
@@ -774,6 +1008,21 @@ extern "C" int pcops_knn_ws(const float *q, const float *p, int B, int S, int N,
                                      (hipStream_t)stream);
     if (r < 0) return PCOPS_ERR_LAUNCH;
     if (r > 0) return PCOPS_OK;
+  }
+  static const bool c3 = [] {  // PCOPS_KNN_C3=0: knnC2_kernel (A/B)
+    const char *e = getenv("PCOPS_KNN_C3");
+    return !(e && e[0] == '0');
+  }();
+  const int kk = K + pad;
+  if (c3 && C >= 32 && (C & 3) == 0 && kk <= 32 && workspace && workspace_bytes >= knnC3_bytes(B, S, N, kk) && !knn_v1()) {
+    hipStream_t st = (hipStream_t)stream;
+    switch (kk_of(kk)) {
+      case 4: return launch_knnC3<4>(q, p, B, S, N, C, K, pad, idx, dist, workspace, st);
+      case 8: return launch_knnC3<8>(q, p, B, S, N, C, K, pad, idx, dist, workspace, st);
+      case 16: return launch_knnC3<16>(q, p, B, S, N, C, K, pad, idx, dist, workspace, st);
+      case 20: return launch_knnC3<20>(q, p, B, S, N, C, K, pad, idx, dist, workspace, st);
+      default: return launch_knnC3<32>(q, p, B, S, N, C, K, pad, idx, dist, workspace, st);
+    }
   }
   return pcops_knn(q, p, B, S, N, C, K, pad, idx, dist, stream);
 }

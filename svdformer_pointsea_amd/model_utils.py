@@ -40,7 +40,9 @@ def _knn(q, p, k, pad=0, want_dist=False):
     dist = torch.empty(B, S, k, dtype=torch.float32, device=q.device) if want_dist else None
     with torch.cuda.device(q.device):
         wsb = lib().pcops_knn_workspace_bytes(B, S, N, C, k + pad) if _KNN_SORTED else 0
-        if wsb:   # C == 3: the Morton-ordered scan (knn.hip knn3s_kernel), same result bit for bit
+        # with scratch: C == 3 by the Morton-ordered scan (knn3s_kernel), C >= 32 by the streamed,
+        # candidate-split form (knnC3_kernel); both give the index-order scan's result bit for bit
+        if wsb:
             ws = Workspace.get(q.device, wsb)
             call("knn", lib().pcops_knn_ws, ptr(q), ptr(p), B, S, N, C, k, pad, ptr(idx), ptr(dist), ptr(ws), wsb,
                  stream_of(q))
@@ -49,7 +51,7 @@ def _knn(q, p, k, pad=0, want_dist=False):
     return (idx, dist) if want_dist else idx
 
 
-_KNN_SORTED = os.environ.get("PCOPS_KNN_SORTED", "1") != "0"   # A/B switch
+_KNN_SORTED = os.environ.get("PCOPS_KNN_SORTED", "1") != "0"   # A/B switch: 0 = pcops_knn (no scratch)
 
 
 def query_knn(nsample, xyz, new_xyz, include_self=True):

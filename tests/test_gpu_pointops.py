@@ -623,3 +623,34 @@ def test_knn_sorted_scan_bitexact(dev, monkeypatch, case):
         oidx, od = O.knn(qn, p, K, pad, return_dist=True)
         np.testing.assert_array_equal(got[0].cpu().numpy(), oidx)
         np.testing.assert_array_equal(got[1].cpu().numpy(), od)
+
+
+@pytest.mark.parametrize("B,S,N,C,K,pad,kind", [(32, 512, 512, 64, 8, 0, "rand"), (16, 1024, 1024, 256, 4, 0, "rand"),
+                                                 (16, 1024, 1024, 64, 8, 0, "tiled"), (2, 300, 300, 40, 5, 2, "rand"),
+                                                 (3, 200, 777, 128, 20, 1, "tiled"), (2, 1000, 100, 32, 16, 0, "rand"),
+                                                 (1, 64, 4000, 96, 32, 0, "rand")])
+def test_knn_feature_split_bitexact(dev, monkeypatch, B, S, N, C, K, pad, kind):
+    """The streamed, candidate-split feature-space kNN (knnC3_kernel + knn_merge_kernel) against
+    knnC2_kernel (pcops_knn): idx and dist bitwise at the model shapes (PCN gcn_2, PointSea
+    gcn_2 / gcn_3), with exact ties (duplicated rows), pad, more queries than candidates, and
+    empty trailing splits; the oracle on the small cases."""
+    import svdformer_pointsea_amd.model_utils as MU
+
+    rng = np.random.default_rng(B * S + N + C)
+    if kind == "tiled":
+        u = rng.standard_normal((B, max(8, N // 5), C)).astype(np.float32)
+        p = u[:, rng.integers(0, u.shape[1], N)]
+    else:
+        p = rng.standard_normal((B, N, C)).astype(np.float32)
+    q = p[:, :S].copy() if S <= N else rng.standard_normal((B, S, C)).astype(np.float32)
+    pt = T(p, dev)
+    qt = pt if S == N else T(q, dev)
+    got = MU._knn(qt, pt, K, pad, want_dist=True)
+    monkeypatch.setattr(MU, "_KNN_SORTED", False)
+    ref = MU._knn(qt, pt, K, pad, want_dist=True)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    if B * S * N <= 4_000_000:
+        oidx, od = O.knn(q, p, K, pad, return_dist=True)
+        np.testing.assert_array_equal(got[0].cpu().numpy(), oidx)
+        np.testing.assert_array_equal(got[1].cpu().numpy(), od)
