@@ -420,241 +420,6 @@ __global__ __launch_bounds__(256) void knnC2_kernel(const float *__restrict__ q,
                          dist ? dist + ((size_t)b * S + sc) * K : nullptr);
 }
 
-// ----------------------------------------------------------------- C == 3, spatially ordered scan
-// The buffered selection above costs 2-3x the distances (tools/knn_bench.py with the
-// selection ablated: gcn_1's 2048 x 2048 self-kNN 0.180 -> 0.056 ms): with candidates in index
-// order -- random in space -- a lane's list threshold falls slowly and ~70 candidates per lane
-// pass it.  Here both clouds are first sorted by the Morton code of the candidate cloud's
-// bounding box (knn_morton_kernel), a block takes 64 consecutive sorted queries (spatially
-// compact) and scans the candidate tiles starting at the tile where its queries' codes fall,
-// then outward: after the first tile the thresholds are nearly final.  Every candidate is
-// still scanned and compared as (distance, index) pairs -- insertion, filter and the wave
-// merge are lexicographic -- so the result is the index-order scan's whatever the order.
-__device__ __forceinline__ unsigned part1by2(unsigned v) {  // 10 bits -> every third bit
-  v &= 0x3ff;
-  v = (v | (v << 16)) & 0x030000ff;
-  v = (v | (v << 8)) & 0x0300f00f;
-  v = (v | (v << 4)) & 0x030c30c3;
-  v = (v | (v << 2)) & 0x09249249;
-  return v;
-}
-
-// One block per batch: points of `pts` (n of them) sorted by (Morton code in the bounding box
-// of `box` (nb points), index), written as float4 (x, y, z, (x*x + y*y) + z*z), the original
-// index and the code.  Bitonic sort of NMAX 64-bit keys in LDS (keys unique: the index).
-template <int NMAX>
-__global__ __launch_bounds__(1024) void knn_morton_kernel(const float *__restrict__ pts, int n,
-                                                          const float *__restrict__ box, int nb,
-                                                          float4 *__restrict__ out_pt, int *__restrict__ out_idx,
-                                                          unsigned *__restrict__ out_code) {
-  __shared__ unsigned long long key[NMAX];
-  __shared__ float red[6][16];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const float *P = pts + (size_t)b * n * 3, *Q = box + (size_t)b * nb * 3;
-  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (int i = tid; i < nb; i += 1024)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float v = Q[3 * i + c];
-      lo[c] = fminf(lo[c], v);
-      hi[c] = fmaxf(hi[c], v);
-    }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    lo[c] = wave_min_f32(lo[c]);
-    hi[c] = wave_max_f32(hi[c]);
-  }
-  if ((tid & 63) == 0)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      red[c][tid >> 6] = lo[c];
-      red[3 + c][tid >> 6] = hi[c];
-    }
-  __syncthreads();
-  float org[3], sc[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    float a = red[c][0], z = red[3 + c][0];
-    for (int w = 1; w < 16; ++w) {
-      a = fminf(a, red[c][w]);
-      z = fmaxf(z, red[3 + c][w]);
-    }
-    org[c] = a;
-    const float ext = z - a;
-    sc[c] = ext > 0.f && ext < INFINITY ? 1023.f / ext : 0.f;
-  }
-  for (int i = tid; i < NMAX; i += 1024) {
-    unsigned long long k = ~0ull;
-    if (i < n) {
-      unsigned code = 0;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        float t = (P[3 * i + c] - org[c]) * sc[c];
-        t = t > 0.f ? (t < 1023.f ? t : 1023.f) : 0.f;  // NaN -> 0
-        code |= part1by2((unsigned)t) << c;
-      }
-      k = ((unsigned long long)code << 32) | (unsigned)i;
-    }
-    key[i] = k;
-  }
-  __syncthreads();
-  for (int kk = 2; kk <= NMAX; kk <<= 1)
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < NMAX; i += 1024) {
-        const int l = i ^ j;
-        if (l > i) {
-          const unsigned long long a = key[i], c = key[l];
-          const bool up = (i & kk) == 0;
-          if ((a > c) == up) {
-            key[i] = c;
-            key[l] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  for (int i = tid; i < n; i += 1024) {
-    const unsigned long long k = key[i];
-    const int o = (int)(unsigned)(k & 0xffffffffu);
-    const float x = P[3 * o], y = P[3 * o + 1], z = P[3 * o + 2];
-    out_pt[(size_t)b * n + i] = make_float4(x, y, z, (x * x + y * y) + z * z);
-    out_idx[(size_t)b * n + i] = o;
-    out_code[(size_t)b * n + i] = (unsigned)(k >> 32);
-  }
-}
-
-// (distance, index) lexicographic top-KK insertion: the list stays sorted by the pair
-template <int KK>
-__device__ __forceinline__ void topk_insert_lex(float (&bd)[KK], int (&bi)[KK], float d, int k) {
-  if (d < bd[KK - 1] || (d == bd[KK - 1] && k < bi[KK - 1])) {
-    bd[KK - 1] = d;
-    bi[KK - 1] = k;
-#pragma unroll
-    for (int s = KK - 1; s > 0; --s) {
-      const bool sw = bd[s] < bd[s - 1] || (bd[s] == bd[s - 1] && bi[s] < bi[s - 1]);
-      const float d0 = bd[s - 1], d1 = bd[s];
-      const int i0 = bi[s - 1], i1 = bi[s];
-      bd[s - 1] = sw ? d1 : d0;
-      bd[s] = sw ? d0 : d1;
-      bi[s - 1] = sw ? i1 : i0;
-      bi[s] = sw ? i0 : i1;
-    }
-  }
-}
-
-template <int KK, int CAP, int NT>
-struct TopKLex {
-  float bd[KK];
-  int bi[KK];
-  float thr;
-  int thi;
-  int cnt;
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int k = 0; k < KK; ++k) {
-      bd[k] = INFINITY;
-      bi[k] = INT_MAX;
-    }
-    thr = INFINITY;
-    thi = INT_MAX;
-    cnt = 0;
-  }
-  // an infinite distance never enters (as in TopK's strict filter against the initial +inf)
-  __device__ __forceinline__ void offer(int2 *queue, int tid, float d, int k) {
-    if (d < thr || (d == thr && k < thi && d < INFINITY)) {
-      queue[cnt * NT + tid] = make_int2(__float_as_int(d), k);
-      ++cnt;
-    }
-  }
-  __device__ __forceinline__ void drain(const int2 *queue, int tid) {
-    for (int j = 0; __any(j < cnt); ++j) {
-      if (j < cnt) {
-        const int2 v = queue[j * NT + tid];
-        topk_insert_lex<KK>(bd, bi, __int_as_float(v.x), v.y);
-      }
-    }
-    thr = bd[KK - 1];
-    thi = bi[KK - 1];
-    cnt = 0;
-  }
-  __device__ __forceinline__ void maybe_drain(const int2 *queue, int tid, int room) {
-    if (__any(cnt > CAP - room)) drain(queue, tid);
-  }
-};
-
-template <int KK, int G, int TN>
-__global__ __launch_bounds__(64 * G) void knn3s_kernel(const float4 *__restrict__ ps, const int *__restrict__ pidx,
-                                                       const unsigned *__restrict__ pcode,
-                                                       const float4 *__restrict__ qs, const int *__restrict__ qidx,
-                                                       const unsigned *__restrict__ qcode, int S, int N, int K,
-                                                       int pad, int *__restrict__ idx, float *__restrict__ dist) {
-  constexpr int SL = TN / G, U = 8, CAP = 12, NT = 64 * G;  // CAP 12: 34 KB, 4 blocks / CU
-  __shared__ float4 tile[TN];
-  __shared__ int tix[TN];
-  __shared__ int start;
-  __shared__ union {
-    MergeBuf<KK, G> mb;
-    int2 queue[CAP * NT];
-  } sh;
-  const int b = blockIdx.y, tid = threadIdx.x;
-  const int w = tid >> 6, lane = tid & 63;
-  const int j = blockIdx.x * 64 + lane;  // sorted query position
-  const int jc = j < S ? j : S - 1;
-  const float4 *P = ps + (size_t)b * N;
-  const int *PI = pidx + (size_t)b * N;
-  const float4 qv = qs[(size_t)b * S + jc];
-  const float qx = qv.x, qy = qv.y, qz = qv.z, qn = qv.w;
-  const float mx = -2.f * qx, my = -2.f * qy, mz = -2.f * qz;
-  if (tid == 0) {  // the candidate position of the block's middle query code
-    const unsigned c = qcode[(size_t)b * S + min((int)blockIdx.x * 64 + 32, S - 1)];
-    const unsigned *pc = pcode + (size_t)b * N;
-    int lo = 0, hi = N;
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if (pc[m] < c) lo = m + 1;
-      else hi = m;
-    }
-    start = lo;
-  }
-  __syncthreads();
-  const int nt = (N + TN - 1) / TN;
-  // tiles centred on the start position, then outward: [t0, t0+1, t0-1, t0+2, ...]
-  const int t0 = min(max(0, start - TN / 2), max(0, N - TN)) / TN;
-  TopKLex<KK, CAP, NT> tk;
-  tk.init();
-  int up = t0, dn = t0 - 1;
-  for (int it = 0; it < nt; ++it) {
-    int t;
-    if (up < nt && (dn < 0 || (it & 1) == 0)) t = up++;
-    else t = dn--;
-    const int c0 = t * TN, cnt = min(TN, N - c0);
-    for (int e = tid; e < cnt; e += NT) {
-      tile[e] = P[c0 + e];
-      tix[e] = PI[c0 + e];
-    }
-    __syncthreads();
-    const int e1 = min(cnt, (w + 1) * SL);
-    for (int e0 = w * SL; e0 < e1; e0 += U) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = e0 + u;
-        if (e < e1) {
-          const float4 c = tile[e];
-          const float dot = __builtin_fmaf(mz, c.z, __builtin_fmaf(my, c.y, mx * c.x));
-          tk.offer(sh.queue, tid, (dot + qn) + c.w, tix[e]);
-        }
-      }
-      tk.maybe_drain(sh.queue, tid, U);
-    }
-    __syncthreads();
-  }
-  tk.drain(sh.queue, tid);
-  const int qo = qidx[(size_t)b * S + jc];
-  merge_and_store<KK, G>(sh.mb, tk.bd, tk.bi, w, lane, j < S, K, pad, N, idx + ((size_t)b * S + qo) * K,
-                         dist ? dist + ((size_t)b * S + qo) * K : nullptr);
-}
-
-// candidates (float4, index, code), then the queries' (S == 0: self kNN, shared)
 // ----------------------------------------------------------------- C >= 32, streamed (v3)
 // knnC2_kernel's arithmetic (4x4 register micro-tile, each distance a sequential fma chain over
 // the channels in order, then ((-2 dot) + |q|^2) + |p|^2 with torch_sumsq norms) with the
@@ -843,60 +608,6 @@ __global__ __launch_bounds__(256) void knn_merge_kernel(const float *__restrict_
   }
 }
 
-size_t knn_sorted_bytes(int B, int S, int N) {
-  auto a = [](size_t x) { return (x + 255) & ~size_t(255); };
-  auto part = [&](int n) { return a((size_t)B * n * 16) + 2 * a((size_t)B * n * 4); };
-  return part(N) + (S > 0 ? part(S) : 0);
-}
-
-// C == 3, KK <= 16, N and S <= 4096: the sorted form (0 = not applicable)
-int launch_knn3_sorted(const float *q, const float *p, int B, int S, int N, int K, int pad, int *idx, float *dist,
-                       void *ws, size_t wsb, hipStream_t st) {
-  static const bool on = [] {
-    const char *e = getenv("PCOPS_KNN_SORTED");
-    return !(e && e[0] == '0');
-  }();
-  if (!on || !ws || N > 4096 || S > 4096 || K + pad > 16) return 0;
-  const bool self = q == p && S == N;
-  const size_t need = knn_sorted_bytes(B, self ? 0 : S, N);  // (the C-ABI sizes for S > 0)
-  if (wsb < need) return 0;
-  auto a = [](size_t x) { return (x + 255) & ~size_t(255); };
-  char *w = (char *)ws;
-  float4 *pp = (float4 *)w;
-  w += a((size_t)B * N * 16);
-  int *pi = (int *)w;
-  w += a((size_t)B * N * 4);
-  unsigned *pc = (unsigned *)w;
-  w += a((size_t)B * N * 4);
-  float4 *qp = pp;
-  int *qi = pi;
-  unsigned *qc = pc;
-  auto sort = [&](const float *src, int n, float4 *o, int *oi, unsigned *oc) {
-    if (n <= 2048)
-      hipLaunchKernelGGL(knn_morton_kernel<2048>, dim3(B), dim3(1024), 0, st, src, n, p, N, o, oi, oc);
-    else
-      hipLaunchKernelGGL(knn_morton_kernel<4096>, dim3(B), dim3(1024), 0, st, src, n, p, N, o, oi, oc);
-  };
-  sort(p, N, pp, pi, pc);
-  if (!self) {
-    qp = (float4 *)w;
-    w += a((size_t)B * S * 16);
-    qi = (int *)w;
-    w += a((size_t)B * S * 4);
-    qc = (unsigned *)w;
-    sort(q, S, qp, qi, qc);
-  }
-  const dim3 grid((S + 63) / 64, B);
-  if ((long)grid.x * grid.y < 768)
-    hipLaunchKernelGGL((knn3s_kernel<16, 8, 1024>), grid, dim3(512), 0, st, pp, pi, pc, qp, qi, qc, S, N, K, pad,
-                       idx, dist);
-  else
-    hipLaunchKernelGGL((knn3s_kernel<16, 4, 512>), grid, dim3(256), 0, st, pp, pi, pc, qp, qi, qc, S, N, K, pad, idx,
-                       dist);
-  if (hipGetLastError() != hipSuccess) return -1;
-  return 1;
-}
-
 bool knn_v1() {  // PCOPS_KNN_V1=1: the first-generation feature-space kernel (A/B runs)
   static const bool v = [] {
     const char *e = getenv("PCOPS_KNN_V1");
@@ -987,7 +698,6 @@ int launch_knnC3(const float *q, const float *p, int B, int S, int N, int C, int
 
 extern "C" unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int C, int K) {
   if (B <= 0 || S <= 0 || N <= 0 || C <= 0 || K <= 0) return 0;
-  if (C == 3) return knn_sorted_bytes(B, S, N);
   if (C >= 32 && C <= 512 && K <= 32) return knnC3_bytes(B, S, N, K);
   return 0;
 }
@@ -995,20 +705,14 @@ extern "C" unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int
 extern "C" int pcops_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx,
                          float *dist, pcops_stream_t stream);
 
-// pcops_knn with scratch: C == 3 (K + pad <= 16, S and N <= 4096) takes the Morton-ordered
-// scan (knn3s_kernel); every other case, or a short workspace, is pcops_knn
+// pcops_knn with scratch: C >= 32 (C % 4 == 0, K + pad <= 32) takes the streamed, candidate-split
+// form (knnC3_kernel + knn_merge_kernel); every other case, or a short workspace, is pcops_knn
 extern "C" int pcops_knn_ws(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx,
                             float *dist, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream) {
   if (B < 0 || S < 0 || N < 0 || C <= 0 || K < 0 || pad < 0 || C > 512) return PCOPS_ERR_INVALID;
   if (B == 0 || S == 0 || K == 0) return PCOPS_OK;
   if (!q || !p || !idx || N <= 0) return PCOPS_ERR_INVALID;
   if (K + pad > N) return PCOPS_ERR_INVALID;
-  if (C == 3) {
-    const int r = launch_knn3_sorted(q, p, B, S, N, K, pad, idx, dist, workspace, workspace_bytes,
-                                     (hipStream_t)stream);
-    if (r < 0) return PCOPS_ERR_LAUNCH;
-    if (r > 0) return PCOPS_OK;
-  }
   static const bool c3 = [] {  // PCOPS_KNN_C3=0: knnC2_kernel (A/B)
     const char *e = getenv("PCOPS_KNN_C3");
     return !(e && e[0] == '0');

@@ -564,67 +564,6 @@ def test_pcsa_kernel_matches_torch_chain(dev, dtype, K, C):
         torch.testing.assert_close(a.float(), b.float(), rtol=tol * 5, atol=tol * 5)
 
 
-@pytest.mark.parametrize("case", ["self2048", "query512", "tiled", "flat", "line", "n4096", "n4097", "s_gt_n",
-                                  "tiny", "pad1", "nan"])
-def test_knn_sorted_scan_bitexact(dev, monkeypatch, case):
-    """The Morton-ordered C = 3 scan (pcops_knn_ws, knn3s_kernel) against the index-order
-    scan (pcops_knn) and the oracle: idx and dist bitwise, incl. exact ties (duplicated
-    points), degenerate bounding boxes, the self-kNN form (q is p), sizes at and past the
-    4096 limit, more queries than candidates, pad and a NaN point."""
-    import svdformer_pointsea_amd.model_utils as MU
-
-    rng = np.random.default_rng(len(case) * 31)
-    B, K, pad = 2, 16, 0
-    if case == "self2048":
-        p = (rng.random((32, 2048, 3)) - 0.5).astype(np.float32)
-        q = None
-    elif case == "query512":
-        p = rng.standard_normal((4, 2048, 3)).astype(np.float32)
-        q = p[:, rng.permutation(2048)[:512]].copy()
-    elif case == "tiled":
-        p = _tiled(rng, B, 150, 2048)
-        q = None
-    elif case == "flat":
-        p = (rng.random((B, 1500, 3)) - 0.5).astype(np.float32)
-        p[..., 2] = 0.25
-        q = p[:, :700].copy()
-    elif case == "line":
-        p = np.zeros((B, 1000, 3), np.float32)
-        p[..., 0] = np.linspace(-1, 1, 1000, dtype=np.float32)
-        q = None
-    elif case == "n4096":
-        p = rng.standard_normal((B, 4096, 3)).astype(np.float32)
-        q = p[:, :1000].copy()
-    elif case == "n4097":
-        p = rng.standard_normal((B, 4097, 3)).astype(np.float32)
-        q = p[:, :300].copy()
-    elif case == "s_gt_n":
-        p = rng.standard_normal((B, 300, 3)).astype(np.float32)
-        q = rng.standard_normal((B, 900, 3)).astype(np.float32)
-    elif case == "tiny":
-        p = rng.standard_normal((B, 20, 3)).astype(np.float32)
-        q, K = None, 8
-    elif case == "pad1":
-        p = rng.standard_normal((B, 2048, 3)).astype(np.float32)
-        q, K, pad = None, 15, 1
-    else:
-        p = rng.standard_normal((B, 1024, 3)).astype(np.float32)
-        p[0, 17] = np.nan
-        q = p[:, ::3].copy()
-    pt = T(p, dev)
-    qt = pt if q is None else T(q, dev)
-    qn = p if q is None else q
-    got = MU._knn(qt, pt, K, pad, want_dist=True)
-    monkeypatch.setattr(MU, "_KNN_SORTED", False)
-    ref = MU._knn(qt, pt, K, pad, want_dist=True)
-    for a, b in zip(got, ref):
-        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
-    if case != "nan" and qn.shape[0] * qn.shape[1] <= 4096:
-        oidx, od = O.knn(qn, p, K, pad, return_dist=True)
-        np.testing.assert_array_equal(got[0].cpu().numpy(), oidx)
-        np.testing.assert_array_equal(got[1].cpu().numpy(), od)
-
-
 @pytest.mark.parametrize("B,S,N,C,K,pad,kind", [(32, 512, 512, 64, 8, 0, "rand"), (16, 1024, 1024, 256, 4, 0, "rand"),
                                                  (16, 1024, 1024, 64, 8, 0, "tiled"), (2, 300, 300, 40, 5, 2, "rand"),
                                                  (3, 200, 777, 128, 20, 1, "tiled"), (2, 1000, 100, 32, 16, 0, "rand"),
