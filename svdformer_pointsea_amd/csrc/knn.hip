@@ -196,11 +196,16 @@ template <int KK, int G, int TN>
 __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
                                                       int N, int K, int pad, int *__restrict__ idx,
                                                       float *__restrict__ dist) {
-  constexpr int SL = TN / G, U = 8, CAP = 16, NT = 64 * G;
+  // CAP 15 leaves room for the shared thresholds inside the merge buffer's footprint
+  // (40 KB at G = 4, TN = 512: four blocks per CU)
+  constexpr int SL = TN / G, U = 8, CAP = 15, NT = 64 * G;
   __shared__ float4 tile[TN];
   __shared__ union {
     MergeBuf<KK, G> mb;
-    int2 queue[CAP * NT];
+    struct {
+      int2 queue[CAP * NT];
+      float sthr[G][64];
+    } sc;
   } sh;
   const int b = blockIdx.y, tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
@@ -213,6 +218,16 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
   const float mx = -2.f * qx, my = -2.f * qy, mz = -2.f * qz;  // (-2q).p == -2(q.p) bit-exactly
   TopK<KK, CAP, NT> tk;
   tk.init();
+  // Shared thresholds: a candidate farther than ANY wave's current KK-th distance for this
+  // query cannot be in the merged top KK (that wave already holds KK closer ones), so each
+  // wave also filters against the others' published thresholds -- the G lists then converge
+  // like one list over G times the candidates instead of G lists each built from scratch
+  // (the selection was ~70 % of the kernel, profiles/r4_knn_ab.txt).  Ties (d equal to the
+  // other wave's threshold) still pass, and a stale threshold is only a looser filter, so
+  // the merged result is exactly the unfiltered one.  Relaxed LDS atomics, no barrier.
+  float(&sthr)[G][64] = sh.sc.sthr;
+  __hip_atomic_store(&sthr[w][lane], INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  float xthr = INFINITY;
   for (int t0 = 0; t0 < N; t0 += TN) {
     const int cnt = min(TN, N - t0);
     for (int e = tid; e < cnt; e += NT) {
@@ -234,17 +249,24 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
           const float dd = (dot + qn) + c.w;
           if (dd < tk.bd[0]) { tk.bd[0] = dd; tk.bi[0] = t0 + e; }
 #else
-          tk.offer(sh.queue, tid, (dot + qn) + c.w, t0 + e);
+          const float d = (dot + qn) + c.w;
+          if (d <= xthr) tk.offer(sh.sc.queue, tid, d, t0 + e);
 #endif
         }
       }
 #if !PCOPS_KNN_ABL
-      tk.maybe_drain(sh.queue, tid, U);
+      tk.maybe_drain(sh.sc.queue, tid, U);
+      if constexpr (G > 1) {
+        __hip_atomic_store(&sthr[w][lane], tk.thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (g != w) xthr = fminf(xthr, __hip_atomic_load(&sthr[g][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      }
 #endif
     }
     __syncthreads();
   }
-  tk.drain(sh.queue, tid);
+  tk.drain(sh.sc.queue, tid);
   merge_and_store<KK, G>(sh.mb, tk.bd, tk.bi, w, lane, s < S, K, pad, N, idx + ((size_t)b * S + sc) * K,
                          dist ? dist + ((size_t)b * S + sc) * K : nullptr);
 }
