@@ -3,8 +3,10 @@ pointsea) train step under a TorchDispatchMode that records every aten op outsid
 libpcops / GEMM / conv calls (copies, casts, cat, elementwise, reductions, fills) with
 its output + input bytes and the innermost Python frame in svdformer_pointsea_amd/ or
 bench.py.  Backward ops of torch's own autograd nodes have no Python frame: they are
-charged to "<autograd>" plus the op.  Prints GB and calls per site (complements
-tools/glue_ops.py, whose profiler stacks come back empty on this torch build)."""
+charged to "<autograd>" plus the op -- or, with --nodes, to the autograd node running when
+they are issued (a gradient-accumulation add is issued while its PRODUCER runs) and that
+node's forward site (anomaly mode records it; slower, same ops).  Prints GB and calls per
+site (complements tools/glue_ops.py, whose profiler stacks come back empty on this torch build)."""
 import argparse
 import os
 import sys
@@ -23,6 +25,7 @@ from svdformer_pointsea_amd.train import FlatParams  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="svdformer")
 ap.add_argument("--rows", type=int, default=60)
+ap.add_argument("--nodes", action="store_true", help="attribute backward ops to the running autograd node")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.backends.cudnn.benchmark = True
@@ -49,12 +52,29 @@ def nbytes(x):
     return 0
 
 
+def ours(f):
+    return "svdformer_pointsea_amd" in f or f.endswith("bench.py") or "/metrics" in f
+
+
+def node_site():
+    node = torch._C._current_autograd_node()
+    if node is None:
+        return "<autograd>"
+    tb = node.metadata.get("traceback_", []) if hasattr(node, "metadata") else []
+    site = "?"
+    for entry in (tb if isinstance(tb, list) else [tb]):  # formatted frames, outermost first
+        head = entry.strip().splitlines()[0] if entry.strip() else ""
+        parts = head.split('"')   # File "<path>", line N, in <fn>
+        if head.startswith("File ") and len(parts) >= 3 and ours(parts[1]):
+            site = f"{os.path.basename(parts[1])}:{parts[2].split(',')[1].split()[-1]}"
+    return f"<{node.name()} @ {site}>"
+
+
 def frame():
-    for fr in reversed(traceback.extract_stack()[:-3]):
-        f = fr.filename
-        if "svdformer_pointsea_amd" in f or f.endswith("bench.py") or "/metrics" in f:
-            return f"{os.path.basename(f)}:{fr.lineno} {fr.name}"
-    return "<autograd>"
+    for fr in reversed(traceback.extract_stack()[:-2]):
+        if ours(fr.filename):
+            return f"{os.path.basename(fr.filename)}:{fr.lineno} {fr.name}"
+    return node_site() if args.nodes else "<autograd>"
 
 
 class Rec(TorchDispatchMode):
@@ -92,6 +112,8 @@ for _ in range(2):
     step()
 torch.cuda.synchronize()
 rec = Rec()
+if args.nodes:
+    torch.autograd.set_detect_anomaly(True, check_nan=False)
 with rec:
     step()
 torch.cuda.synchronize()
