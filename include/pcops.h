@@ -299,6 +299,16 @@ int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *
                                int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
                                float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
                                void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+/* pcops_layernorm_bwd_bf16g: pcops_layernorm_bwd(_colsum) with BOTH upstream gradients bf16:
+ *   dy = dy_a + dy16, dy_a the gradient of the fp32 output y32 as a bf16 consumer produced it
+ *   (the block sum bf16(y32 + f): replaces widening it to fp32 in a separate pass; the sum is
+ *   the same fp32 value bit for bit).  dsum = NULL: no column sum (workspace
+ *   pcops_layernorm_bwd_workspace_bytes), else as pcops_layernorm_bwd_colsum (its workspace).
+ *   Replaces the autograd cast in front of nn.LayerNorm's backward (models/model_utils.py:600-617). */
+int pcops_layernorm_bwd_bf16g(const void *dy_a, const void *dy16, const void *a, int a_dtype, const void *b,
+                              int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
+                              float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
+                              void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_gelu_bwd_colsum: du = dy * GELU'(u) (exact erf GELU, torch's GeluBackward expression in
  *   fp32) over a row-major (rows, C) matrix, dy / u / du all `dtype` (0 fp32, 1 bf16), C % 8 == 0;
  *   when dsum != NULL also dsum[c] = sum_r du[r][c] over du as stored (C fp32): the bias gradient

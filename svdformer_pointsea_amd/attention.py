@@ -521,8 +521,11 @@ class _LayerNorm(Function):
         a, b, w, mean, rstd = ctx.saved_tensors
         C = a.shape[-1]
         rows = a.numel() // C
-        g32 = None if g32 is None else g32.contiguous().float()
+        ga16 = _take_g16(g32)   # y32's gradient as the bf16 block sum handed it down (_AddToBf16)
         g16 = None if g16 is None else g16.contiguous().to(torch.bfloat16)
+        if ga16 is not None and g16 is None:
+            ga16, g32 = None, ga16.float()
+        g32 = None if (g32 is None or ga16 is not None) else g32.contiguous().float()
         dtypes = {a.dtype} | ({b.dtype} if b is not None else set())
         dx32 = torch.empty(a.shape, dtype=torch.float32, device=a.device) if torch.float32 in dtypes else None
         dx16 = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device) if torch.bfloat16 in dtypes else None
@@ -530,7 +533,17 @@ class _LayerNorm(Function):
         db = torch.empty_like(dw)
         src = None if ctx.sum_of is None else (a, b)[ctx.sum_of]
         need = (ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        if src is not None and need[ctx.sum_of]:
+        if ga16 is not None:   # both upstream gradients bf16: widened inside the launch
+            dsum = torch.empty_like(dw) if (src is not None and need[ctx.sum_of]) else None
+            wsb = (lib().pcops_layernorm_bwd_colsum_workspace_bytes(rows, C) if dsum is not None
+                   else lib().pcops_layernorm_bwd_workspace_bytes(rows, C))
+            ws = _lib.Workspace.get(a.device, wsb)
+            with torch.cuda.device(a.device):
+                call("layernorm_bwd", lib().pcops_layernorm_bwd_bf16g, ptr(ga16), ptr(g16), ptr(a), _dt(a), ptr(b),
+                     0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16),
+                     ptr(dw), ptr(db), ptr(dsum), _DT[src.dtype] if dsum is not None else 0, ptr(ws), wsb,
+                     stream_of(a))
+        elif src is not None and need[ctx.sum_of]:
             dsum = torch.empty_like(dw)
             wsb = lib().pcops_layernorm_bwd_colsum_workspace_bytes(rows, C)
             ws = _lib.Workspace.get(a.device, wsb)
@@ -659,14 +672,46 @@ class _BlockBase(nn.Module):
         return layer_norm(self.norm13, y, sum_of=0 if hasattr(self, "input_proj") else None)
 
 
+# The bf16 gradient of a LayerNorm's fp32 output, handed from _AddToBf16.backward to
+# _LayerNorm.backward without the widening pass autograd would otherwise run (2 GB of
+# casts per PCN step).  Autograd insists on an fp32 gradient for the fp32 output, so
+# the hand-off returns a stride-0 view of a NaN scalar carrying the bf16 tensor; the
+# LayerNorm backward reads the bf16 tensor.  Only taken when the sum is the LayerNorm
+# output's only consumer (the blocks' residual stream s2); if autograd ever had to add
+# another gradient to it, the NaN poisons the sum loudly instead of dropping a term.
+_LN_G16 = os.environ.get("PCOPS_LN_G16", "1") != "0"   # A/B switch
+_NAN_SCALAR = {}
+
+
+def _g16_handoff(g, shape):
+    dev = g.device
+    nan = _NAN_SCALAR.get(dev)
+    if nan is None:
+        nan = _NAN_SCALAR[dev] = torch.full((), float("nan"), dtype=torch.float32, device=dev)
+    fake = nan.expand(shape)
+    fake._pcops_g16 = g.contiguous()
+    return fake
+
+
+def _take_g16(g):
+    if g is None:
+        return None
+    h = getattr(g, "_pcops_g16", None)
+    if h is not None:
+        del g._pcops_g16
+    return h
+
+
 class _AddToBf16(Function):
     """bf16(a + b) in one kernel for a block output that only feeds GEMMs:
     the same value autocast would produce from the fp32 sum (one rounding),
     without materialising the fp32 sum; backward casts the bf16 gradient once
-    (a's dtype) instead of widening it and narrowing it again."""
+    (a's dtype) instead of widening it and narrowing it again -- or, when a is a
+    LayerNorm's fp32 output read by nothing else (single_use), hands the bf16
+    gradient to that LayerNorm's backward uncast (_g16_handoff)."""
 
     @staticmethod
-    def forward(ctx, a, b):
+    def forward(ctx, a, b, single_use=False):
         out = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
         if _PCOPS_ADD and a.shape == b.shape and a.dtype in _DT and b.dtype in _DT:
             a, b = a.contiguous(), b.contiguous()
@@ -675,12 +720,19 @@ class _AddToBf16(Function):
         else:   # broadcasting (never in the models): torch's add
             torch.add(a, b, out=out)
         ctx.dts = (a.dtype, b.dtype)
+        fn = a.grad_fn
+        ctx.handoff = (single_use and _LN_G16 and a.dtype == torch.float32 and fn is not None
+                       and type(fn).__name__ == "_LayerNormBackward" and a.output_nr == 0)
+        ctx.shape = a.shape
         return out
 
     @staticmethod
     def backward(ctx, g):
+        gb = g.to(ctx.dts[1])
+        if ctx.handoff and g.dtype == torch.bfloat16:
+            return _g16_handoff(g, ctx.shape), gb, None
         ga = g.to(ctx.dts[0])
-        return ga, (ga if ctx.dts[1] == ctx.dts[0] else g.to(ctx.dts[1]))
+        return ga, (ga if ctx.dts[1] == ctx.dts[0] else gb), None
 
 
 class PosEmbedding:
@@ -719,10 +771,11 @@ class _AddPosBf16(Function):
         return g.to(ctx.sdt), None, None
 
 
-def block_sum(s, f):
+def block_sum(s, f, single_use=False):
     """s + f of a block's (residual, FFN) outputs whose consumers are GEMMs
     (input_proj / conv_ps): bf16 directly under bf16 autocast, else s + f.
-    f may be a PosEmbedding (the SDG query's positional term)."""
+    f may be a PosEmbedding (the SDG query's positional term).  single_use: s is
+    a block tail's LayerNorm output that nothing else reads (see _AddToBf16)."""
     if isinstance(f, PosEmbedding):
         if (_PCOPS_POSEMB and _want_bf16() and s.is_cuda and s.dim() == 3 and s.shape[-1] % 8 == 0
                 and s.dtype in _DT):
@@ -730,7 +783,7 @@ def block_sum(s, f):
             return _AddPosBf16.apply(s, f.cd, div)
         f = f.tensor()
     if _BLOCK_SUM16 and _want_bf16() and s.is_cuda:
-        return _AddToBf16.apply(s, f)
+        return _AddToBf16.apply(s, f, single_use)
     return s + f
 
 
@@ -827,8 +880,8 @@ class SDG_Decoder(nn.Module):
 
     def forward_tokens(self, x_tok):
         s, f = self.sa1.forward_tokens(x_tok)
-        s, f = self.sa2.forward_tokens(block_sum(s, f))   # sa2 starts with input_proj (a GEMM)
-        return block_sum(s, f)                             # SDG feeds it to input_proj / conv_ps
+        s, f = self.sa2.forward_tokens(block_sum(s, f, True))   # sa2 starts with input_proj (a GEMM)
+        return block_sum(s, f, True)                             # SDG feeds it to input_proj / conv_ps
 
     def forward(self, input):
         s, f = self.sa1.forward_tokens(to_tokens(input))

@@ -177,7 +177,8 @@ int ln_bwd_rpw(int rows) {
 
 // CH: 8-element chunks per lane (1 for C <= 512, 2 for C <= 1024); AT / BT as
 // the forward; GM: which upstream gradients are present (1 = dy32, 2 = dy16,
-// 3 both); CS: also the column sums of dx (the bias gradient of the Linear
+// 3 both; 7 = both, the first one bf16 too: the fp32 output's gradient as the bf16
+// block sum handed it down, widened here instead of by a separate cast pass); CS: also the column sums of dx (the bias gradient of the Linear
 // whose output is a or b) over the values as stored -- bf16-rounded when
 // sum16 -- as a third C-wide partial row.
 template <int CH, int AT, int BT, int GM, bool CS>
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
       const long long e = base + 8 * min(lane + 64 * i, nch - 1);
       ld8c<AT>(xh[i], a, e);
       if constexpr (BT >= 0) ld8c<BT>(t[i], b, e);
-      if constexpr (GM & 1) ld8c<0>(u[i], g32, e);
+      if constexpr (GM & 1) ld8c<(GM & 4) ? 1 : 0>(u[i], g32, e);
       if constexpr (GM & 2) ld8c<1>(v[i], g16, e);
     }
     float sg = 0.f, sgx = 0.f;
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
         float x = xh[i].v[k];
         if constexpr (BT >= 0) x += t[i].v[k];
         float d;
-        if constexpr (GM == 3)
+        if constexpr ((GM & 3) == 3)
           d = u[i].v[k] + v[i].v[k];
         else if constexpr (GM == 1)
           d = u[i].v[k];
@@ -340,7 +341,9 @@ struct LnFwdF {
 template <int CH, int AT, int BT>
 struct LnBwdF {
   static void go(const LnArgs &p, int gm, int blocks, int rpw) {
-    if (gm == 3)
+    if (gm == 7)
+      ln_bwd_go<CH, AT, BT, 7>(p, blocks, rpw);
+    else if (gm == 3)
       ln_bwd_go<CH, AT, BT, 3>(p, blocks, rpw);
     else if (gm == 1)
       ln_bwd_go<CH, AT, BT, 1>(p, blocks, rpw);
@@ -913,7 +916,8 @@ namespace {
 int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b, int b_dtype,
                        const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
                        void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src, void *workspace,
-                       unsigned long long workspace_bytes, unsigned long long need, hipStream_t s) {
+                       unsigned long long workspace_bytes, unsigned long long need, hipStream_t s,
+                       bool dy32_bf16 = false) {
   if (rows < 0 || C <= 0) return PCOPS_ERR_INVALID;
   if (C > 512 * kMaxCh || C % 8) return PCOPS_ERR_UNSUPPORTED;
   if (!dgamma || !dbeta) return PCOPS_ERR_INVALID;
@@ -948,8 +952,8 @@ int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a
   p.cs = dsum != nullptr;
   p.sum16 = dsum_src == 1;
   p.s = s;
-  ln_dispatch<LnBwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p, (dy32 ? 1 : 0) | (dy16 ? 2 : 0), blocks,
-                      ln_bwd_rpw(rows));
+  ln_dispatch<LnBwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p,
+                      (dy32 ? 1 : 0) | (dy16 ? 2 : 0) | (dy32_bf16 ? 4 : 0), blocks, ln_bwd_rpw(rows));
   const int np = dsum ? 3 : 2;
   launch_colsum_final(part, blocks, np * C, (void *)dgamma, 0, C, (void *)dbeta, 2 * C, (void *)dsum, s);
   PC_CHECK_LAUNCH();
@@ -980,6 +984,19 @@ extern "C" int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, c
   return layernorm_bwd_impl(dy32, dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, dx16, dgamma, dbeta,
                             dsum, dsum_src, workspace, workspace_bytes,
                             pcops_layernorm_bwd_colsum_workspace_bytes(rows, C), (hipStream_t)stream);
+}
+
+extern "C" int pcops_layernorm_bwd_bf16g(const void *dy_a, const void *dy16, const void *a, int a_dtype,
+                                         const void *b, int b_dtype, const float *gamma, const float *mean,
+                                         const float *rstd, int rows, int C, float *dx32, void *dx16, float *dgamma,
+                                         float *dbeta, float *dsum, int dsum_src, void *workspace,
+                                         unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (!dy_a || !dy16) return PCOPS_ERR_INVALID;
+  return layernorm_bwd_impl((const float *)dy_a, dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, dx16,
+                            dgamma, dbeta, dsum, dsum_src, workspace, workspace_bytes,
+                            dsum ? pcops_layernorm_bwd_colsum_workspace_bytes(rows, C)
+                                 : pcops_layernorm_bwd_workspace_bytes(rows, C),
+                            (hipStream_t)stream, true);
 }
 
 extern "C" unsigned long long pcops_colsum_workspace_bytes(long long rows, int C) {

@@ -93,6 +93,7 @@ _SA_FUSED = _os.environ.get("PCOPS_SA_FUSED", "1") != "0"
 _MAXK = _os.environ.get("PCOPS_MAXK", "1") != "0"   # A/B switch: pcops_max_k for the neighbourhood max
 # PCOPS_EDGE_FUSED=0: EdgeConv's unfused group_local -> repeat -> subtract -> cat path (A/B, parity tests)
 _EDGE_FUSED = _os.environ.get("PCOPS_EDGE_FUSED", "1") != "0"
+_PS_ROWS = _os.environ.get("PCOPS_PS_ROWS", "1") != "0"   # A/B switch: SDG upsampling rows straight from conv_ps
 
 
 def max_over_neighbours_tokens(x):
@@ -469,7 +470,7 @@ class SDG(nn.Module):
         if isinstance(dec, SDG_Decoder):
             return dec.forward_tokens(x)
         s, f = dec.forward_tokens(x)
-        return block_sum(s, f)
+        return block_sum(s, f, True)
 
     def forward_tokens(self, local_tok, coarse, f_g, partial):
         """Token-major SDG: local_tok (B,512,C), coarse (B,N,3), f_g (B,512,1),
@@ -485,19 +486,40 @@ class SDG(nn.Module):
         # (B,N,hidden).reshape(B,hidden,N).permute(2,0,1) of the reference, token-major
         pos = PosEmbedding(half_cd, self.embedding, self.hidden)   # added inside the q / k input
         s, f = self.sa1.forward_tokens(F_, pos)
-        F_Q = block_sum(s, f)   # feeds decoder1 / cross1, both starting with input_proj
+        F_Q = block_sum(s, f, True)   # feeds decoder1 / cross1, both starting with input_proj
         F_Q_ = self._decode(self.decoder1, F_Q)
         # similarity alignment with the local features
         local = _lin(self.mlpp.mlp[2], self.mlpp.mlp[1](_lin(self.mlpp.mlp[0], local_tok)))
         s, f = self.cross1.forward_tokens(F_Q, local)
-        F_H_ = self._decode(self.decoder2, block_sum(s, f))
-        T = _lin(self.conv_ps, torch.cat([F_Q_.to(F_H_.dtype), F_H_], dim=-1))
-        # (B, C*r, N).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n
+        F_H_ = self._decode(self.decoder2, block_sum(s, f, True))
+        Tin = torch.cat([F_Q_.to(F_H_.dtype), F_H_], dim=-1)
+        # (B, C*r, N).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n.
         r = self.ratio
+        if _PS_ROWS:
+            # conv_ps's output channels taken in (j, c) order instead, so its output IS the
+            # upsampled rows, point (n, j) at row n*r + j, without the transposing copy (and
+            # its copy back in backward); the per-point layers run in that row order and the
+            # sum with the repeated coarse points writes the reference order j*N + n
+            perm = self._ps_perm(Tin.device)
+            w = self.conv_ps.weight.view(self.conv_ps.weight.shape[0], -1)
+            F_L = linear(Tin, w.index_select(0, perm), self.conv_ps.bias.index_select(0, perm))
+            F_L = _lin(self.conv_delta, F_L.view(B, N * r, -1))
+            O_L = _lin(self.conv_out, self.relu(_lin(self.conv_out1, F_L)))
+            return (coarse.unsqueeze(2) + O_L.view(B, N, r, -1)).transpose(1, 2).reshape(B, r * N, -1)
+        T = _lin(self.conv_ps, Tin)
         F_L = T.reshape(B, N, -1, r).permute(0, 3, 1, 2).reshape(B, r * N, -1)
         F_L = _lin(self.conv_delta, F_L)
         O_L = _lin(self.conv_out, self.relu(_lin(self.conv_out1, F_L)))
         return coarse.repeat(1, r, 1) + O_L
+
+    def _ps_perm(self, dev):
+        """perm[j*C + c] = c*r + j over conv_ps's C*r output channels."""
+        key = str(dev)
+        cache = self.__dict__.setdefault("_ps_perm_cache", {})
+        if key not in cache:
+            C, r = self.conv_ps.weight.shape[0] // self.ratio, self.ratio
+            cache[key] = torch.arange(C * r, device=dev).view(C, r).t().reshape(-1)
+        return cache[key]
 
 
 # PCOPS_IMG_STREAM=1: the image branch on a third stream beside the point branch.  Off: same-box PCN

@@ -966,3 +966,40 @@ def test_add_posemb_kernel(dev, B, N, H, sdt):
     g = torch.randn(B, N, H, generator=gen).to(dev, torch.bfloat16)
     got.backward(g)
     assert s.grad.dtype == sdt and torch.equal(s.grad, g.to(sdt))
+
+
+@pytest.mark.parametrize("L,C,Cout", [(512, 256, 256), (2048, 512, 512), (300, 128, 256)])
+def test_block_sum_g16_handoff_bitwise(dev, monkeypatch, L, C, Cout):
+    """The bf16 gradient of the block tail's LayerNorm output handed to its backward uncast
+    (_AddToBf16 -> pcops_layernorm_bwd_bf16g) against the widening cast + pcops_layernorm_bwd:
+    input and parameter gradients bitwise equal (fp32(a) + fp32(b) in the kernel is the same
+    value as the pre-widened sum).  Second part: if the LayerNorm output also had another
+    consumer, the hand-off must poison the gradient (NaN), never drop a term."""
+    import svdformer_pointsea_amd.attention as A
+
+    torch.manual_seed(L + C)
+    blk = A.self_attention(C, Cout, nhead=8).to(dev)
+    x0 = torch.randn(2, L, C, device=dev)
+    g = torch.randn(2, L, Cout, device=dev).to(torch.bfloat16)
+
+    def run(handoff):
+        monkeypatch.setattr(A, "_LN_G16", handoff)
+        blk.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            s, f = blk.forward_tokens(x)
+            y = A.block_sum(s, f, True)
+        y.backward(g)
+        return [x.grad.clone()] + [p.grad.clone() for p in blk.parameters()]
+
+    got, ref = run(True), run(False)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+    monkeypatch.setattr(A, "_LN_G16", True)
+    x = x0.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        s, f = blk.forward_tokens(x)
+        y = A.block_sum(s, f, True)        # claims single use ...
+        z = (s * 2).sum()                  # ... but s has a second reader
+    (y.float() * g.float()).sum().add(z).backward()
+    assert torch.isnan(x.grad).any()

@@ -593,3 +593,58 @@ def test_knn_feature_split_bitexact(dev, monkeypatch, B, S, N, C, K, pad, kind):
         oidx, od = O.knn(q, p, K, pad, return_dist=True)
         np.testing.assert_array_equal(got[0].cpu().numpy(), oidx)
         np.testing.assert_array_equal(got[1].cpu().numpy(), od)
+
+
+@pytest.mark.parametrize("B,S,N,K,pad,kind", [(32, 2048, 2048, 16, 0, "surface"), (32, 512, 2048, 16, 0, "fps"),
+                                              (4, 1024, 1024, 16, 1, "tiled"), (3, 333, 1500, 8, 1, "cluster"),
+                                              (2, 700, 700, 20, 0, "flat"), (2, 300, 300, 16, 0, "nan"),
+                                              (2, 100, 17, 16, 1, "surface"), (2, 256, 4096, 32, 0, "far"),
+                                              (1, 2000, 64, 4, 0, "line"), (8, 640, 640, 16, 0, "zero")])
+def test_knn3_seeded_bitexact(dev, monkeypatch, B, S, N, K, pad, kind):
+    """C = 3 kNN seeded from candidate cells (knn_cells_kernel + knn3_kernel's window bound) against
+    the unseeded scan (pcops_knn) and the oracle: idx and dist bitwise.  Clouds that stress the
+    bound: exact duplicates (ties at the bound), tight clusters far apart, a flat cloud (zero extent
+    along z), NaN points, N = K + pad, queries far outside the candidates' box, points on a line,
+    an all-zero cloud."""
+    import svdformer_pointsea_amd.model_utils as MU
+
+    rng = np.random.default_rng(B * S + N + K)
+    if kind in ("surface", "fps", "nan", "far"):
+        v = rng.standard_normal((B, N, 3)).astype(np.float32)
+        p = (v / np.linalg.norm(v, axis=-1, keepdims=True)).astype(np.float32)
+    elif kind == "tiled":
+        u = rng.random((B, N // 8, 3), dtype=np.float32)
+        p = u[:, rng.integers(0, u.shape[1], N)]
+    elif kind == "cluster":
+        c = rng.standard_normal((B, 5, 3)).astype(np.float32) * 10
+        p = (c[:, rng.integers(0, 5, N)] + 1e-3 * rng.standard_normal((B, N, 3))).astype(np.float32)
+    elif kind == "flat":
+        p = rng.random((B, N, 3), dtype=np.float32)
+        p[..., 2] = 0.5
+    elif kind == "line":
+        t = rng.random((B, N, 1), dtype=np.float32)
+        p = (t * np.array([1.0, 2.0, -0.5], np.float32)).astype(np.float32)
+    else:
+        p = np.zeros((B, N, 3), np.float32)
+    if kind == "nan":
+        p[:, ::37] = np.nan
+    p = np.ascontiguousarray(p)
+    if kind == "fps":
+        q = p[:, rng.permutation(N)[:S]].copy()
+    elif kind == "far":
+        q = (rng.standard_normal((B, S, 3)) * 50).astype(np.float32)
+    elif S <= N:
+        q = p[:, :S].copy()
+    else:
+        q = rng.random((B, S, 3), dtype=np.float32)
+    pt = T(p, dev)
+    qt = pt if (S == N and kind not in ("fps", "far")) else T(q, dev)
+    got = MU._knn(qt, pt, K, pad, want_dist=True)
+    monkeypatch.setattr(MU, "_KNN_SORTED", False)
+    ref = MU._knn(qt, pt, K, pad, want_dist=True)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+    if B * S * N <= 4_000_000 and kind != "nan":
+        oidx, od = O.knn(q, p, K, pad, return_dist=True)
+        np.testing.assert_array_equal(got[0].cpu().numpy(), oidx)
+        np.testing.assert_array_equal(got[1].cpu().numpy(), od)

@@ -1,9 +1,12 @@
 set -o pipefail
-O=gpurun_out/r4m; mkdir -p $O
-export PYTEST_K="knn or group_local or edgeconv or add_posemb"
+O=gpurun_out/r4q; mkdir -p $O
+export TMPDIR=/tmp
+export PYTEST_K="knn"
 bash tools/gpu_run.sh $O tests_k || exit 1
-for i in 1 2; do
-  timeout -k 10 120 python tools/knn_bench.py > $O/knn_c3_$i.txt 2>&1 || exit 1
-  PCOPS_KNN_C3=0 timeout -k 10 120 python tools/knn_bench.py > $O/knn_c2_$i.txt 2>&1 || exit 1
+for cfg in "1 1" "0 1" "1 0" "0 0"; do
+  set -- $cfg
+  PCOPS_KNN_SEED=$1 PCOPS_KNN_SHARE=$2 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
+    -d $O/prof_s$1_h$2 -o run -- python tools/knn_bench.py > $O/knn_s$1_h$2.txt 2>&1 || exit 1
+  f=$(find $O/prof_s$1_h$2 -name '*kernel_stats.csv' -print -quit); cp "$f" $O/stats_s$1_h$2.csv
+  find $O/prof_s$1_h$2 -name '*kernel_trace.csv' -delete
 done
-bash tools/gpu_run.sh $O bench_ps
