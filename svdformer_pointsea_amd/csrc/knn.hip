@@ -705,10 +705,18 @@ __global__ __launch_bounds__(256) void knnC3_kernel(const float *__restrict__ q,
       __syncthreads();
       const int e1 = min(CT, n1 - t0);
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int e = w * 16 + kk;
-        if (e < e1) tk.offer(sh.queue, t, sd[lane][e], t0 + e);
-        if (kk == 7 || kk == 15) tk.maybe_drain(sh.queue, t, 8);
+      for (int h = 0; h < 2; ++h) {
+        // 8 distances read first, together (inside the offer branches each read waited alone:
+        // the compiler cannot move it above a queue write); columns past e1 hold clamped rows
+        float dv[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) dv[kk] = sd[lane][w * 16 + 8 * h + kk];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const int e = w * 16 + 8 * h + kk;
+          if (e < e1) tk.offer(sh.queue, t, dv[kk], t0 + e);
+        }
+        tk.maybe_drain(sh.queue, t, 8);
       }
       __syncthreads();    // the distance tile is read before the next step's query chunk lands
     }
