@@ -1020,5 +1020,7 @@ def test_gelu_fwd_kernel_bitwise(dev, n, dtype):
     y = torch.empty_like(x)
     call("gelu_fwd", lib().pcops_gelu_fwd, ptr(x), 0 if dtype == torch.float32 else 1, n, ptr(y), stream_of(x))
     ref = F.gelu(x)
-    assert torch.equal(y.view(torch.int16 if dtype == torch.bfloat16 else torch.int32),
-                       ref.view(torch.int16 if dtype == torch.bfloat16 else torch.int32))
+    nan = torch.isnan(ref)
+    assert torch.equal(torch.isnan(y), nan)   # NaN payloads may differ; everything else bit for bit
+    it = torch.int16 if dtype == torch.bfloat16 else torch.int32
+    assert torch.equal(y[~nan].view(it), ref[~nan].view(it))
