@@ -188,101 +188,6 @@ struct TopK {
   }
 };
 
-// Candidate cells for the C == 3 seed (knn_cells_kernel): the candidate cloud's box cut into
-// 16^3 cells, the candidates counting-sorted by the cell's Morton code.  geom[b] = (lo.xyz,
-// scale.xyz), cstart[b][c] = first sorted position of cell c (cstart[b][4096] = N),
-// perm[b][j] = index of the j-th sorted candidate.  The order INSIDE a cell comes from LDS
-// atomics and may differ run to run: it only moves the seed threshold, never the result.
-constexpr int kCellBits = 4, kCells = 1 << (3 * kCellBits);
-
-__device__ __forceinline__ int cell_axis(float x, float lo, float sc) {
-  const float t = fminf(fmaxf((x - lo) * sc, 0.f), float((1 << kCellBits) - 1));  // NaN -> 0
-  return (int)t;
-}
-__device__ __forceinline__ int cell_of(float x, float y, float z, const float *g) {
-  const int cx = cell_axis(x, g[0], g[3]), cy = cell_axis(y, g[1], g[4]), cz = cell_axis(z, g[2], g[5]);
-  int code = 0;
-#pragma unroll
-  for (int bit = 0; bit < kCellBits; ++bit)
-    code |= (((cx >> bit) & 1) << (3 * bit)) | (((cy >> bit) & 1) << (3 * bit + 1)) | (((cz >> bit) & 1) << (3 * bit + 2));
-  return code;
-}
-
-__global__ __launch_bounds__(1024) void knn_cells_kernel(const float *__restrict__ p, int N, float *__restrict__ geom,
-                                                         int *__restrict__ cstart, int *__restrict__ perm) {
-  __shared__ int cnt[kCells];
-  __shared__ float red[6][16];
-  __shared__ float g[6];
-  __shared__ int wsum[16];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float *pb = p + (size_t)b * N * 3;
-  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int i = tid; i < N; i += 1024) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const float x = pb[3 * i + a];
-      v[a] = fminf(v[a], x);  // NaN ignored
-      v[3 + a] = fmaxf(v[3 + a], x);
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 6; ++a) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float u = __shfl_xor(v[a], o);
-      v[a] = a < 3 ? fminf(v[a], u) : fmaxf(v[a], u);
-    }
-    if (lane == 0) red[a][w] = v[a];
-  }
-  for (int c = tid; c < kCells; c += 1024) cnt[c] = 0;
-  __syncthreads();
-  if (tid < 3) {
-    float lo = red[tid][0], hi = red[3 + tid][0];
-    for (int j = 1; j < 16; ++j) {
-      lo = fminf(lo, red[tid][j]);
-      hi = fmaxf(hi, red[3 + tid][j]);
-    }
-    const float ext = hi - lo;
-    const bool ok = ext > 0.f && ext < INFINITY;  // else every point in cell 0 along this axis
-    g[tid] = ok ? lo : 0.f;
-    g[3 + tid] = ok ? float(1 << kCellBits) / ext : 0.f;
-  }
-  __syncthreads();
-  if (tid < 6) geom[(size_t)b * 8 + tid] = g[tid];
-  for (int i = tid; i < N; i += 1024) atomicAdd(&cnt[cell_of(pb[3 * i], pb[3 * i + 1], pb[3 * i + 2], g)], 1);
-  __syncthreads();
-  // exclusive scan of the 4096 counts: 4 per thread, wave prefix by shuffles, then the 16 waves
-  constexpr int PT = kCells / 1024;
-  int loc[PT], run = 0;
-#pragma unroll
-  for (int j = 0; j < PT; ++j) {
-    loc[j] = run;
-    run += cnt[tid * PT + j];
-  }
-  int incl = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(incl, o);
-    if (lane >= o) incl += u;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int base = incl - run;
-  for (int j = 0; j < w; ++j) base += wsum[j];
-  int *cs = cstart + (size_t)b * (kCells + 1);
-#pragma unroll
-  for (int j = 0; j < PT; ++j) {
-    cnt[tid * PT + j] = base + loc[j];  // becomes the running insert position
-    cs[tid * PT + j] = base + loc[j];
-  }
-  if (tid == 0) cs[kCells] = N;
-  __syncthreads();
-  for (int i = tid; i < N; i += 1024) {
-    const int pos = atomicAdd(&cnt[cell_of(pb[3 * i], pb[3 * i + 1], pb[3 * i + 2], g)], 1);
-    perm[(size_t)b * N + pos] = i;
-  }
-}
-
 // C == 3: candidates staged as float4 (x, y, z, |p|^2), TN per tile.
 // Large grids (>= 3 blocks per CU): G = 4, TN = 512 -> 40 KB of LDS, so four
 // blocks (16 waves) fit a CU and the whole grid is resident at once; small
@@ -290,9 +195,7 @@ __global__ __launch_bounds__(1024) void knn_cells_kernel(const float *__restrict
 template <int KK, int G, int TN>
 __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ q, const float *__restrict__ p, int S,
                                                       int N, int K, int pad, int *__restrict__ idx,
-                                                      float *__restrict__ dist, const float *__restrict__ geom,
-                                                      const int *__restrict__ cstart, const int *__restrict__ perm,
-                                                      bool share) {
+                                                      float *__restrict__ dist, bool share) {
   // CAP 15 leaves room for the shared thresholds inside the merge buffer's footprint
   // (40 KB at G = 4, TN = 512: four blocks per CU)
   constexpr int SL = TN / G, U = 8, CAP = 15, NT = 64 * G;
@@ -325,32 +228,6 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
   float(&sthr)[G][64] = sh.sc.sthr;
   __hip_atomic_store(&sthr[w][lane], INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   float xthr = INFINITY;
-  // Seed (with candidate cells): the K + pad candidates around the query's cell in Morton order
-  // are K + pad real candidates, so the largest of their distances -- evaluated exactly as the
-  // scan evaluates them -- bounds the (K + pad)-th smallest from above.  Candidates beyond it
-  // cannot be selected; ties with it still pass ('<='), so the result is the unseeded one bit
-  // for bit, whatever the bound.  A NaN distance in the window leaves the bound at +inf.
-  if (geom && K + pad <= N) {
-    const int W = K + pad;
-    const float *g = geom + (size_t)b * 8;
-    const int *cs = cstart + (size_t)b * (kCells + 1);
-    const int c = cell_of(qx, qy, qz, g);
-    const int lo = cs[c], hi = cs[c + 1];
-    const int w0 = min(max(lo + ((hi - lo) >> 1) - (W >> 1), 0), N - W);
-    const int *pp = perm + (size_t)b * N + w0;
-    float T = -INFINITY;
-    bool nan = false;
-    for (int j = 0; j < W; ++j) {
-      const float *src = pb + (size_t)pp[j] * 3;
-      const float x = src[0], y = src[1], z = src[2];
-      const float cw = (x * x + y * y) + z * z;
-      const float dot = __builtin_fmaf(mz, z, __builtin_fmaf(my, y, mx * x));
-      const float d = (dot + qn) + cw;
-      nan |= d != d;
-      T = fmaxf(T, d);
-    }
-    xthr = nan ? INFINITY : T;
-  }
   for (int t0 = 0; t0 < N; t0 += TN) {
     const int cnt = min(TN, N - t0);
     for (int e = tid; e < cnt; e += NT) {
@@ -784,30 +661,24 @@ bool knn_share_on() {  // PCOPS_KNN_SHARE=0: no cross-wave threshold sharing (A/
   return v;
 }
 
-// seed: candidate cells from knn_cells_kernel (C == 3 with scratch), or null
-struct Seed {
-  const float *geom = nullptr;
-  const int *cstart = nullptr, *perm = nullptr;
-};
-
 template <int KK>
 int launch_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
-               hipStream_t st, Seed sd = Seed{}) {
+               hipStream_t st) {
   constexpr int G = KK <= 16 ? 4 : (KK <= 32 ? 2 : 1);
   const dim3 grid((S + 63) / 64, B);
   if (C == 3) {
     if constexpr (KK <= 16) {
       if ((long)grid.x * grid.y < 768) {  // < 3 blocks per CU: more waves per query
         hipLaunchKernelGGL((knn3_kernel<KK, 8, 1024>), grid, dim3(512), 0, st, q, p, S, N, K, pad, idx, dist,
-                           sd.geom, sd.cstart, sd.perm, knn_share_on());
+                           knn_share_on());
         PC_CHECK_LAUNCH();
         return PCOPS_OK;
       }
-      hipLaunchKernelGGL((knn3_kernel<KK, 4, 512>), grid, dim3(256), 0, st, q, p, S, N, K, pad, idx, dist, sd.geom,
-                         sd.cstart, sd.perm, knn_share_on());
+      hipLaunchKernelGGL((knn3_kernel<KK, 4, 512>), grid, dim3(256), 0, st, q, p, S, N, K, pad, idx, dist,
+                         knn_share_on());
     } else {
       hipLaunchKernelGGL((knn3_kernel<KK, G, 1024>), grid, dim3(64 * G), 0, st, q, p, S, N, K, pad, idx, dist,
-                         sd.geom, sd.cstart, sd.perm, knn_share_on());
+                         knn_share_on());
     }
     PC_CHECK_LAUNCH();
     return PCOPS_OK;
@@ -873,22 +744,8 @@ int launch_knnC3(const float *q, const float *p, int B, int S, int N, int C, int
   return PCOPS_OK;
 }
 
-// C == 3 scratch: per batch the cell geometry (8 floats), the cell starts and the sorted order
-size_t knn_seed_bytes(int B, int N) {
-  auto a = [](size_t x) { return (x + 255) & ~size_t(255); };
-  return a((size_t)B * 8 * 4) + a((size_t)B * (kCells + 1) * 4) + a((size_t)B * N * 4);
-}
-bool knn_seed_on() {  // PCOPS_KNN_SEED=0: unseeded C == 3 scan (A/B)
-  static const bool v = [] {
-    const char *e = getenv("PCOPS_KNN_SEED");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 extern "C" unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int C, int K) {
   if (B <= 0 || S <= 0 || N <= 0 || C <= 0 || K <= 0) return 0;
-  if (C == 3 && K <= 64) return knn_seed_bytes(B, N);
   if (C >= 32 && C <= 512 && K <= 32) return knnC3_bytes(B, S, N, K);
   return 0;
 }
@@ -896,10 +753,9 @@ extern "C" unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int
 extern "C" int pcops_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx,
                          float *dist, pcops_stream_t stream);
 
-// pcops_knn with scratch: C == 3 seeds each query's threshold from candidate cells
-// (knn_cells_kernel, then knn3_kernel); C >= 32 (C % 4 == 0, K + pad <= 32) takes the streamed,
-// candidate-split form (knnC3_kernel + knn_merge_kernel); every other case, or a short
-// workspace, is pcops_knn.  Same output as pcops_knn bit for bit.
+// pcops_knn with scratch: C >= 32 (C % 4 == 0, K + pad <= 32) takes the streamed, candidate-split
+// form (knnC3_kernel + knn_merge_kernel); every other case, or a short workspace, is pcops_knn.
+// Same output as pcops_knn bit for bit.
 extern "C" int pcops_knn_ws(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx,
                             float *dist, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream) {
   if (B < 0 || S < 0 || N < 0 || C <= 0 || K < 0 || pad < 0 || C > 512) return PCOPS_ERR_INVALID;
@@ -911,28 +767,6 @@ extern "C" int pcops_knn_ws(const float *q, const float *p, int B, int S, int N,
     return !(e && e[0] == '0');
   }();
   const int kk = K + pad;
-  if (C == 3 && kk <= 64 && workspace && workspace_bytes >= knn_seed_bytes(B, N) && knn_seed_on()) {
-    auto a = [](size_t x) { return (x + 255) & ~size_t(255); };
-    hipStream_t st = (hipStream_t)stream;
-    char *w = (char *)workspace;
-    Seed sd;
-    float *geom = (float *)w;
-    w += a((size_t)B * 8 * 4);
-    int *cstart = (int *)w;
-    w += a((size_t)B * (kCells + 1) * 4);
-    int *perm = (int *)w;
-    hipLaunchKernelGGL(knn_cells_kernel, dim3(B), dim3(1024), 0, st, p, N, geom, cstart, perm);
-    PC_CHECK_LAUNCH();
-    sd.geom = geom;
-    sd.cstart = cstart;
-    sd.perm = perm;
-    if (kk <= 4) return launch_knn<4>(q, p, B, S, N, C, K, pad, idx, dist, st, sd);
-    if (kk <= 8) return launch_knn<8>(q, p, B, S, N, C, K, pad, idx, dist, st, sd);
-    if (kk <= 16) return launch_knn<16>(q, p, B, S, N, C, K, pad, idx, dist, st, sd);
-    if (kk <= 20) return launch_knn<20>(q, p, B, S, N, C, K, pad, idx, dist, st, sd);
-    if (kk <= 32) return launch_knn<32>(q, p, B, S, N, C, K, pad, idx, dist, st, sd);
-    return launch_knn<64>(q, p, B, S, N, C, K, pad, idx, dist, st, sd);
-  }
   if (c3 && C >= 32 && (C & 3) == 0 && kk <= 32 && workspace && workspace_bytes >= knnC3_bytes(B, S, N, kk) && !knn_v1()) {
     hipStream_t st = (hipStream_t)stream;
     switch (kk_of(kk)) {

@@ -40,8 +40,8 @@ def _knn(q, p, k, pad=0, want_dist=False):
     dist = torch.empty(B, S, k, dtype=torch.float32, device=q.device) if want_dist else None
     with torch.cuda.device(q.device):
         wsb = lib().pcops_knn_workspace_bytes(B, S, N, C, k + pad) if _KNN_SORTED else 0
-        # with scratch: C == 3 by the Morton-ordered scan (knn3s_kernel), C >= 32 by the streamed,
-        # candidate-split form (knnC3_kernel); both give the index-order scan's result bit for bit
+        # with scratch: C >= 32 by the streamed, candidate-split form (knnC3_kernel + merge),
+        # the index-order scan's result bit for bit
         if wsb:
             ws = Workspace.get(q.device, wsb)
             call("knn", lib().pcops_knn_ws, ptr(q), ptr(p), B, S, N, C, k, pad, ptr(idx), ptr(dist), ptr(ws), wsb,

@@ -23,8 +23,6 @@ Reference map:
   Model                                 PointSea.py:250-272
   SDG_Decoder / self_attention_woinp    models_PointSea/model_utils.py:463-509
 """
-import os
-
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -34,9 +32,7 @@ from .chamfer3D import chamfer_3DDist
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act
 from .pointnet2_utils import furthest_point_sample, gather_operation
-from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin, _NoFork
-
-_LOCAL_FPS_FORK = os.environ.get("PCOPS_LOCAL_FPS_FORK", "1") != "0"
+from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin
 
 
 # ----------------------------------------------------------------- image encoder
@@ -205,12 +201,8 @@ class local_encoder(nn.Module):
         self.local_number = cfg.NETWORK.local_points
 
     def forward(self, inp):
-        # the FPS depends on the input cloud only: on a stream of its own beside gcn_1 (its
-        # 2048 rounds hold B of 256 CUs; PCOPS_LOCAL_FPS_FORK=0 runs it after gcn_1, A/B)
-        with (fork(inp.device, lane=3, inputs=(inp,)) if _LOCAL_FPS_FORK else _NoFork()) as br:
-            idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
         x1 = self.gcn_1(inp)
-        idx = br.join(idx)
+        idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
         x1 = gather_operation(x1.float().contiguous(), idx)
         x2 = self.gcn_2(x1)
         x3 = self.gcn_3(x2)

@@ -600,12 +600,12 @@ def test_knn_feature_split_bitexact(dev, monkeypatch, B, S, N, C, K, pad, kind):
                                               (2, 700, 700, 20, 0, "flat"), (2, 300, 300, 16, 0, "nan"),
                                               (2, 100, 17, 16, 1, "surface"), (2, 256, 4096, 32, 0, "far"),
                                               (1, 2000, 64, 4, 0, "line"), (8, 640, 640, 16, 0, "zero")])
-def test_knn3_seeded_bitexact(dev, monkeypatch, B, S, N, K, pad, kind):
-    """C = 3 kNN seeded from candidate cells (knn_cells_kernel + knn3_kernel's window bound) against
-    the unseeded scan (pcops_knn) and the oracle: idx and dist bitwise.  Clouds that stress the
-    bound: exact duplicates (ties at the bound), tight clusters far apart, a flat cloud (zero extent
-    along z), NaN points, N = K + pad, queries far outside the candidates' box, points on a line,
-    an all-zero cloud."""
+def test_knn3_adversarial_bitexact(dev, monkeypatch, B, S, N, K, pad, kind):
+    """C = 3 kNN (knn3_kernel: batched candidate reads, cross-wave threshold sharing) through both
+    entry points against the oracle: idx and dist bitwise.  Clouds that stress the shared
+    thresholds: exact duplicates (ties at a threshold), tight clusters far apart, a flat cloud,
+    NaN points, N = K + pad, queries far outside the candidates' box, points on a line, an
+    all-zero cloud."""
     import svdformer_pointsea_amd.model_utils as MU
 
     rng = np.random.default_rng(B * S + N + K)
