@@ -182,11 +182,27 @@ struct TopK {
     thr = bd[KK - 1];
     cnt = 0;
   }
+  // branch-free offer: the pair is always written to the lane's next free slot and the
+  // slot is kept only when `pass` (a rejected pair is overwritten by the next one); no
+  // exec-mask branch per candidate -- the VALU -> SALU -> exec chain of a divergent `if`
+  // stalled every candidate step.  The caller has drained so that cnt + pending <= CAP.
+  __device__ __forceinline__ void append(int2 *queue, int tid, float d, int k, bool pass) {
+    queue[cnt * NT + tid] = make_int2(__float_as_int(d), k);
+    cnt += pass ? 1 : 0;
+  }
   // drain when a further `room` offers could overflow some lane's queue
   __device__ __forceinline__ void maybe_drain(const int2 *queue, int tid, int room) {
     if (__any(cnt > CAP - room)) drain(queue, tid);
   }
 };
+
+// smallest float above x (x itself for +inf and NaN)
+__device__ __forceinline__ float next_up(float x) {
+  if (!(x < INFINITY)) return x;
+  if (x == 0.f) return __int_as_float(1);
+  const int b = __float_as_int(x);
+  return __int_as_float(x > 0.f ? b + 1 : b - 1);
+}
 
 // C == 3: candidates staged as float4 (x, y, z, |p|^2), TN per tile.
 // Large grids (>= 3 blocks per CU): G = 4, TN = 512 -> 40 KB of LDS, so four
@@ -227,7 +243,7 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
   // the merged result is exactly the unfiltered one.  Relaxed LDS atomics, no barrier.
   float(&sthr)[G][64] = sh.sc.sthr;
   __hip_atomic_store(&sthr[w][lane], INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  float xthr = INFINITY;
+  float xthr = INFINITY, teff = INFINITY;
   for (int t0 = 0; t0 < N; t0 += TN) {
     const int cnt = min(TN, N - t0);
     for (int e = tid; e < cnt; e += NT) {
@@ -236,32 +252,32 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
       tile[e] = make_float4(x, y, z, (x * x + y * y) + z * z);
     }
     __syncthreads();
-    const int e1 = min(cnt, (w + 1) * SL);  // wave-uniform
-    for (int e0 = w * SL; e0 < e1; e0 += U) {
-      // the U candidates' LDS reads first, all in flight together: read inside the offer
-      // branches, each one was waited for alone (the compiler cannot move a tile read above
-      // a queue write it cannot prove disjoint).  e0 + u < (w + 1) * SL <= TN: in the tile
-      // even past e1 (the last, partial tile), where the offer test below drops them.
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int e1 = min(cnt, (wu + 1) * SL);  // scalar
+    for (int e0 = wu * SL; e0 < e1; e0 += U) {
+      // the U candidates' LDS reads first, all in flight together.  e0 + u < (w + 1) * SL <= TN:
+      // in the tile even past e1 (the last, partial tile), where `live` drops them.
       float4 c[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) c[u] = tile[e0 + u];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = e0 + u;
+        const bool live = e0 + u < e1;  // scalar
         const float dot = __builtin_fmaf(mz, c[u].z, __builtin_fmaf(my, c[u].y, mx * c[u].x));
 #if PCOPS_KNN_ABL
         // diagnostic ablation (tools builds only): distances without the selection
         const float dd = (dot + qn) + c[u].w;
-        if (e < e1 && dd < tk.bd[0]) { tk.bd[0] = dd; tk.bi[0] = t0 + e; }
+        if (live && dd < tk.bd[0]) { tk.bd[0] = dd; tk.bi[0] = t0 + e0 + u; }
 #else
-        const float d = (dot + qn) + c[u].w;
-        if (e < e1 && d <= xthr) tk.offer(sh.sc.queue, tid, d, t0 + e);
+        float d = (dot + qn) + c[u].w;
+        asm volatile("" : "+v"(d));  // keep the chains scalar (SLP paired them into v_pk_* + moves)
+        tk.append(sh.sc.queue, tid, d, t0 + e0 + u, live && d < teff);
 #endif
       }
 #if !PCOPS_KNN_ABL
       tk.maybe_drain(sh.sc.queue, tid, U);
       if (G > 1 && share) {
-        // every wave's threshold, this wave's own included (d <= own is looser than offer's d < own)
+        // every wave's threshold, this wave's own included
         __hip_atomic_store(&sthr[w][lane], tk.thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         float o[G];
 #pragma unroll
@@ -269,6 +285,10 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
 #pragma unroll
         for (int g = 0; g < G; ++g) xthr = __builtin_fminf(xthr, o[g]);
       }
+      // one strict test for both filters: d < own threshold (ties lose to the list's earlier
+      // indices) and d <= any wave's threshold (a tie there may still win on its index), i.e.
+      // d < nextup(xthr); nextup(+inf) = +inf keeps +inf distances out, as the unshared scan does
+      teff = __builtin_fminf(tk.thr, next_up(xthr));
 #endif
     }
     __syncthreads();
@@ -591,7 +611,7 @@ __global__ __launch_bounds__(256) void knnC3_kernel(const float *__restrict__ q,
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
           const int e = w * 16 + 8 * h + kk;
-          if (e < e1) tk.offer(sh.queue, t, dv[kk], t0 + e);
+          tk.append(sh.queue, t, dv[kk], t0 + e, e < e1 && dv[kk] < tk.thr);
         }
         tk.maybe_drain(sh.queue, t, 8);
       }
