@@ -299,10 +299,6 @@ int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *
                                int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
                                float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
                                void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
-/* pcops_gelu_fwd: y = x * 0.5 * (1 + erf(x / sqrt(2))) elementwise over n elements (n % 8 == 0),
- *   x and y `dtype` (0 fp32, 1 bf16), computed in fp32: torch's exact-erf GELU (the blocks' FFN
- *   nn.GELU(), models/model_utils.py:612), bit for bit. */
-int pcops_gelu_fwd(const void *x, int dtype, long long n, void *y, pcops_stream_t stream);
 /* pcops_layernorm_bwd_bf16g: pcops_layernorm_bwd(_colsum) with BOTH upstream gradients bf16:
  *   dy = dy_a + dy16, dy_a the gradient of the fp32 output y32 as a bf16 consumer produced it
  *   (the block sum bf16(y32 + f): replaces widening it to fp32 in a separate pass; the sum is

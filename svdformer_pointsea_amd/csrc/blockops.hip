@@ -400,40 +400,6 @@ void add_go(const void *a, const void *b, void *out, long long n8, hipStream_t s
   hipLaunchKernelGGL((add_kernel<AT, BT, OT>), dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, s, a, b, out, n8);
 }
 
-// ---------------------------------------------------------------- GELU forward
-// y = x * 0.5 * (1 + erf(x * M_SQRT1_2)) in fp32 per element, stored in the input's dtype: the
-// exact-erf nn.GELU() of the blocks' FFN (models/model_utils.py:612), torch's GeluCUDAKernelImpl
-// expression and erf (ocml) -- same bits.  8 elements per thread, 16-B (bf16) / 2x16-B accesses,
-// 4 x 8 in flight per thread (torch's vectorised kernel ran this 1:1 stream at ~4.1 TB/s).
-template <int DT>
-__global__ __launch_bounds__(256) void gelu_fwd_kernel(const void *__restrict__ x, void *__restrict__ y, long long n8) {
-  constexpr int U = 4;
-  const long long stride = (long long)gridDim.x * 256;
-  for (long long i0 = (long long)blockIdx.x * 256 + threadIdx.x; i0 < n8; i0 += stride * U) {
-    V8 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long i = i0 + u * stride;
-      if (i < n8) ld8c<DT>(v[u], x, 8 * i);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long i = i0 + u * stride;
-      if (i < n8) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float a = v[u].v[k];
-          v[u].v[k] = a * 0.5f * (1.0f + erff(a * 0.70710678118654752440f));
-        }
-        if constexpr (DT == 0)
-          st8_f32(reinterpret_cast<float *>(y), 8 * i, v[u]);
-        else
-          st8_bf16(reinterpret_cast<__bf16 *>(y), 8 * i, v[u]);
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------- add + positional embedding
 // out[b][m][h] = a[b][m][h] + E[b][h*N + m], E = SinusoidalPositionalEmbedding(cd) flattened per
 // batch: E[b][n*H + 2i + c] = (c ? cos : sin)(cd[b][n] * div[i])  (models/model_utils.py:883-917,
@@ -899,24 +865,6 @@ extern "C" int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype,
     hipLaunchKernelGGL(add_tail_kernel, dim3(1), dim3(64), 0, s, a, a_dtype, b, b_dtype, out, out_dtype, n8 * 8, n);
     PC_CHECK_LAUNCH();
   }
-  return PCOPS_OK;
-}
-
-extern "C" int pcops_gelu_fwd(const void *x, int dtype, long long n, void *y, pcops_stream_t stream) {
-  if (n < 0 || !dt_ok(dtype)) return PCOPS_ERR_INVALID;
-  if (n == 0) return PCOPS_OK;
-  if (!x || !y) return PCOPS_ERR_INVALID;
-  if (n % 8) return PCOPS_ERR_UNSUPPORTED;
-  const long long n8 = n / 8;
-  long long g = (n8 + 4 * 256 - 1) / (4 * 256);
-  if (g > 8192) g = 8192;
-  if (g < 1) g = 1;
-  hipStream_t s = (hipStream_t)stream;
-  if (dtype == 0)
-    hipLaunchKernelGGL((gelu_fwd_kernel<0>), dim3((unsigned)g), dim3(256), 0, s, x, y, n8);
-  else
-    hipLaunchKernelGGL((gelu_fwd_kernel<1>), dim3((unsigned)g), dim3(256), 0, s, x, y, n8);
-  PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
 

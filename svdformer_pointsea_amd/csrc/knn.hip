@@ -147,7 +147,7 @@ __device__ __forceinline__ void merge_and_store(MergeBuf<KK, G> &mb, const float
 // round instead of once per candidate whenever ANY lane of the wave inserts
 // (with ~5 % of candidates passing per lane, ~95 % of a wave's candidate
 // steps used to pay the whole network).
-#ifndef PCOPS_KNN_ABL
+#ifndef PCOPS_KNN_ABL   // diagnostic builds: 1 = scan only, 2 = scan + filter/append, no insertion
 #define PCOPS_KNN_ABL 0
 #endif
 template <int KK, int CAP, int NT>
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
       for (int u = 0; u < U; ++u) {
         const bool live = e0 + u < e1;  // scalar
         const float dot = __builtin_fmaf(mz, c[u].z, __builtin_fmaf(my, c[u].y, mx * c[u].x));
-#if PCOPS_KNN_ABL
+#if PCOPS_KNN_ABL == 1
         // diagnostic ablation (tools builds only): distances without the selection
         const float dd = (dot + qn) + c[u].w;
         if (live && dd < tk.bd[0]) { tk.bd[0] = dd; tk.bi[0] = t0 + e0 + u; }
@@ -274,8 +274,12 @@ __global__ __launch_bounds__(64 * G) void knn3_kernel(const float *__restrict__ 
         tk.append(sh.sc.queue, tid, d, t0 + e0 + u, live && d < teff);
 #endif
       }
-#if !PCOPS_KNN_ABL
+#if PCOPS_KNN_ABL != 1
+#if PCOPS_KNN_ABL == 2
+      if (__any(tk.cnt > CAP - U)) tk.cnt = 0;  // diagnostic: appends and filters, no insertion
+#else
       tk.maybe_drain(sh.sc.queue, tid, U);
+#endif
       if (G > 1 && share) {
         // every wave's threshold, this wave's own included
         __hip_atomic_store(&sthr[w][lane], tk.thr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
