@@ -669,6 +669,12 @@ class _BlockBase(nn.Module):
         return s2, f
 
     def _in(self, x_tok):
+        if isinstance(x_tok, tuple):
+            # (s, f): the previous block's residual stream and FFN output, whose sum is only this
+            # block's LayerNorm input (no input_proj) -- LN(s + f) in one launch, and f's Linear
+            # gets its bias gradient from the LayerNorm backward
+            assert not hasattr(self, "input_proj")
+            return layer_norm(self.norm13, x_tok[0], x_tok[1], sum_of=1)
         y = _conv1x1_tokens(self.input_proj, x_tok) if hasattr(self, "input_proj") else x_tok
         return layer_norm(self.norm13, y, sum_of=0 if hasattr(self, "input_proj") else None)
 
@@ -772,6 +778,41 @@ class _AddPosBf16(Function):
         return g.to(ctx.sdt), None, None
 
 
+class _Blend(Function):
+    """PointSea's path selection score * a + (1 - score) * b (models_PointSea/PointSea.py:128-131) in one
+    launch each way (pcops_blend_fwd / _bwd), with torch's roundings: the same values and gradients as
+    the four-op expression (score bf16 under autocast, a / b the fp32 residual streams)."""
+
+    @staticmethod
+    def forward(ctx, score, a, b):
+        out = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+        with torch.cuda.device(a.device):
+            call("blend", lib().pcops_blend_fwd, ptr(score), _dt(score), ptr(a), ptr(b), a.numel(), ptr(out),
+                 stream_of(a))
+        ctx.save_for_backward(score, a, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        score, a, b = ctx.saved_tensors
+        g = g.contiguous().float()
+        ds = torch.empty_like(score) if ctx.needs_input_grad[0] else None
+        da = torch.empty_like(a) if ctx.needs_input_grad[1] else None
+        db = torch.empty_like(b) if ctx.needs_input_grad[2] else None
+        with torch.cuda.device(g.device):
+            call("blend_bwd", lib().pcops_blend_bwd, ptr(g), ptr(score), _dt(score), ptr(a), ptr(b), g.numel(),
+                 ptr(da), ptr(db), ptr(ds), stream_of(g))
+        return ds, da, db
+
+
+def blend(score, a, b):
+    """score * a + (1 - score) * b (PointSea's SDG path selection)."""
+    if (_PCOPS_BLEND and score.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32
+            and score.dtype in _DT and score.shape == a.shape == b.shape and a.numel() % 8 == 0):
+        return _Blend.apply(score.contiguous(), a.contiguous(), b.contiguous())
+    return score * a + (1 - score) * b
+
+
 def block_sum(s, f, single_use=False):
     """s + f of a block's (residual, FFN) outputs whose consumers are GEMMs
     (input_proj / conv_ps): bf16 directly under bf16 autocast, else s + f.
@@ -801,6 +842,7 @@ _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnost
 # linear11's bias sum inside the GELU backward (A/B switch); the sum reaches the
 # Linear's backward through _attach_sum / _take_sum (stream-safe hand-off)
 _GELU_SUM = os.environ.get("PCOPS_GELU_SUM", "1") == "1"
+_PCOPS_BLEND = os.environ.get("PCOPS_BLEND", "1") != "0"   # A/B switch: PointSea path selection in one launch
 # in_proj bias sums inside the attention backward passes (A/B switch)
 # the in-pass bias sums exist only in the v2/v3 bf16 kernels: the PCOPS_ATTN_V1 A/B
 # switch (libpcops returns UNSUPPORTED for *_colsum there) takes the plain passes
@@ -899,11 +941,12 @@ class SDG_Decoder_PointSea(nn.Module):
         self.sa2 = self_attention_woinp(hidden_dim, hidden_dim, dropout=dropout, nhead=8)
 
     def forward_tokens(self, x_tok):
+        """x_tok: (B, L, C) or an (s, f) pair whose sum is the input (see _BlockBase._in)."""
         s, f = self.sa1.forward_tokens(x_tok)
-        s, f = self.sa2.forward_tokens(s + f)
+        s, f = self.sa2.forward_tokens((s, f))   # sa2 starts with its LayerNorm
         return s + f
 
     def forward(self, input, pos=None):  # pos is accepted and unused, as in the reference
         s, f = self.sa1.forward_tokens(to_tokens(input))
-        s, f = self.sa2.forward_tokens(s + f)
+        s, f = self.sa2.forward_tokens((s, f))
         return to_channels(s, f, s.dtype)

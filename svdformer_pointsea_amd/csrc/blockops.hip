@@ -400,6 +400,68 @@ void add_go(const void *a, const void *b, void *out, long long n8, hipStream_t s
   hipLaunchKernelGGL((add_kernel<AT, BT, OT>), dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, s, a, b, out, n8);
 }
 
+// ---------------------------------------------------------------- path-selection blend
+// PointSea's SDG path selection F_L = score * F_Q_ + (1 - score) * F_H_ (models_PointSea/PointSea.py:128-131)
+// in one pass each way, reproducing torch's per-op roundings: with a bf16 score (autocast: sigmoid of
+// a Linear output) t2 = bf16(1 - s), out = s * a + t2 * b in fp32; backward da = g * s, db = g * t2 and
+// the score's gradient bf16(bf16(g * a) - bf16(g * b)) -- the two bf16-cast contributions autograd
+// adds (MulBackward for score * F_Q_, RsubBackward of MulBackward for (1 - score) * F_H_).  fp32
+// score: everything fp32.  Replaces 4 forward and ~8 backward elementwise launches.
+template <int ST>
+__device__ __forceinline__ float blend_t2(float s) {
+  const float t = 1.0f - s;
+  return ST == 1 ? (float)(__bf16)t : t;
+}
+
+template <int ST>
+__global__ __launch_bounds__(256) void blend_fwd_kernel(const void *__restrict__ score, const float *__restrict__ a,
+                                                        const float *__restrict__ b, float *__restrict__ out,
+                                                        long long n8) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    V8 sv, av, bv, o;
+    ld8c<ST>(sv, score, 8 * i);
+    ld8c<0>(av, a, 8 * i);
+    ld8c<0>(bv, b, 8 * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float t1 = sv.v[k] * av.v[k];
+      const float t3 = blend_t2<ST>(sv.v[k]) * bv.v[k];
+      o.v[k] = t1 + t3;
+    }
+    st8_f32(out, 8 * i, o);
+  }
+}
+
+template <int ST>
+__global__ __launch_bounds__(256) void blend_bwd_kernel(const float *__restrict__ g, const void *__restrict__ score,
+                                                        const float *__restrict__ a, const float *__restrict__ b,
+                                                        float *__restrict__ da, float *__restrict__ db,
+                                                        void *__restrict__ ds, long long n8) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    V8 gv, sv, av, bv, oa, ob, os;
+    ld8c<0>(gv, g, 8 * i);
+    ld8c<ST>(sv, score, 8 * i);
+    ld8c<0>(av, a, 8 * i);
+    ld8c<0>(bv, b, 8 * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gk = gv.v[k];
+      oa.v[k] = gk * sv.v[k];
+      ob.v[k] = gk * blend_t2<ST>(sv.v[k]);
+      const float u = gk * av.v[k], w = gk * bv.v[k];
+      os.v[k] = ST == 1 ? (float)(__bf16)u - (float)(__bf16)w : u - w;
+    }
+    if (da) st8_f32(da, 8 * i, oa);
+    if (db) st8_f32(db, 8 * i, ob);
+    if (ds) {
+      if constexpr (ST == 1)
+        st8_bf16(reinterpret_cast<__bf16 *>(ds), 8 * i, os);
+      else
+        st8_f32(reinterpret_cast<float *>(ds), 8 * i, os);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- add + positional embedding
 // out[b][m][h] = a[b][m][h] + E[b][h*N + m], E = SinusoidalPositionalEmbedding(cd) flattened per
 // batch: E[b][n*H + 2i + c] = (c ? cos : sin)(cd[b][n] * div[i])  (models/model_utils.py:883-917,
@@ -865,6 +927,47 @@ extern "C" int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype,
     hipLaunchKernelGGL(add_tail_kernel, dim3(1), dim3(64), 0, s, a, a_dtype, b, b_dtype, out, out_dtype, n8 * 8, n);
     PC_CHECK_LAUNCH();
   }
+  return PCOPS_OK;
+}
+
+namespace {
+unsigned blend_grid(long long n8) {
+  long long g = (n8 + 255) / 256;
+  return (unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+}  // namespace
+
+extern "C" int pcops_blend_fwd(const void *score, int score_dtype, const float *a, const float *b, long long n,
+                               float *out, pcops_stream_t stream) {
+  if (n < 0 || !dt_ok(score_dtype)) return PCOPS_ERR_INVALID;
+  if (n == 0) return PCOPS_OK;
+  if (!score || !a || !b || !out) return PCOPS_ERR_INVALID;
+  if (n % 8) return PCOPS_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const long long n8 = n / 8;
+  if (score_dtype == 1)
+    hipLaunchKernelGGL((blend_fwd_kernel<1>), dim3(blend_grid(n8)), dim3(256), 0, s, score, a, b, out, n8);
+  else
+    hipLaunchKernelGGL((blend_fwd_kernel<0>), dim3(blend_grid(n8)), dim3(256), 0, s, score, a, b, out, n8);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_blend_bwd(const float *g, const void *score, int score_dtype, const float *a, const float *b,
+                               long long n, float *da, float *db, void *dscore, pcops_stream_t stream) {
+  if (n < 0 || !dt_ok(score_dtype)) return PCOPS_ERR_INVALID;
+  if (n == 0) return PCOPS_OK;
+  if (!g || !score || !a || !b) return PCOPS_ERR_INVALID;
+  if (n % 8) return PCOPS_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const long long n8 = n / 8;
+  if (score_dtype == 1)
+    hipLaunchKernelGGL((blend_bwd_kernel<1>), dim3(blend_grid(n8)), dim3(256), 0, s, g, score, a, b, da, db, dscore,
+                       n8);
+  else
+    hipLaunchKernelGGL((blend_bwd_kernel<0>), dim3(blend_grid(n8)), dim3(256), 0, s, g, score, a, b, da, db, dscore,
+                       n8);
+  PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
 

@@ -27,7 +27,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import PosEmbedding, SDG_Decoder_PointSea, cross_attention, self_attention, to_tokens
+from .attention import PosEmbedding, SDG_Decoder_PointSea, blend, cross_attention, self_attention, to_tokens
 from .chamfer3D import chamfer_3DDist
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act
@@ -122,14 +122,14 @@ class SDG(nn.Module):
         # similarity alignment
         local = _lin(self.mlpp.mlp[0], local_tok)
         s, f = self.cross1.forward_tokens(F_Q, local)
-        F_H_ = self.decoder2.forward_tokens(s + f)
+        F_H_ = self.decoder2.forward_tokens((s, f))        # its first op is a LayerNorm of s + f
         # path selection
         parts = [F_Q_ + F_H_]
         if self.with_prev:
             parts.append(F_L_prev.to(parts[0].dtype))
         parts += [f_g_current.expand(B, N, -1).to(parts[0].dtype), g.expand(B, N, -1).to(parts[0].dtype)]
         score = torch.sigmoid(_lin(self.fusionMlp.mlp[0], torch.cat(parts, dim=-1)))
-        F_L = score * F_Q_ + (1 - score) * F_H_
+        F_L = blend(score, F_Q_, F_H_)                     # score * F_Q_ + (1 - score) * F_H_
         # conv_ps(F_L).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n
         T = _lin(self.conv_ps, F_L)
         r = self.ratio

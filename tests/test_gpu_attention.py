@@ -1003,3 +1003,51 @@ def test_block_sum_g16_handoff_bitwise(dev, monkeypatch, L, C, Cout):
         z = (s * 2).sum()                  # ... but s has a second reader
     (y.float() * g.float()).sum().add(z).backward()
     assert torch.isnan(x.grad).any()
+
+
+@pytest.mark.parametrize("shape,sdt", [((16, 2048, 512), torch.bfloat16), ((2, 300, 64), torch.bfloat16),
+                                       ((3, 128, 256), torch.float32)])
+def test_blend_bitwise(dev, monkeypatch, shape, sdt):
+    """PointSea's path selection score * a + (1 - score) * b (pcops_blend_fwd / _bwd) against torch's
+    four-op expression: output and the three gradients bitwise (bf16 score: 1 - s rounded to bf16,
+    the score gradient as autograd's two bf16-cast contributions summed in bf16)."""
+    import svdformer_pointsea_amd.attention as A
+
+    torch.manual_seed(shape[-1])
+    s0 = torch.sigmoid(torch.randn(shape, device=dev)).to(sdt)
+    a0, b0 = torch.randn(shape, device=dev) * 3, torch.randn(shape, device=dev)
+    g = torch.randn(shape, device=dev)
+
+    def run(fused):
+        monkeypatch.setattr(A, "_PCOPS_BLEND", fused)
+        s, a, b = (t.clone().requires_grad_(True) for t in (s0, a0, b0))
+        out = A.blend(s, a, b)
+        out.backward(g)
+        return out.detach(), s.grad, a.grad, b.grad
+
+    for x, y in zip(run(True), run(False)):
+        assert x.dtype == y.dtype and torch.equal(x, y)
+
+
+def test_pointsea_decoder_pair_input_bitwise(dev, monkeypatch):
+    """SDG_Decoder_PointSea fed the (s, f) pair (LayerNorm of s + f in one launch, linear12's bias
+    gradient from the LayerNorm backward) against the materialised s + f: outputs, input and parameter
+    gradients bitwise."""
+    import svdformer_pointsea_amd.attention as A
+
+    torch.manual_seed(3)
+    dec = A.SDG_Decoder_PointSea(512, 64, 2).to(dev)
+    s0 = torch.randn(2, 1024, 512, device=dev)
+    f0 = torch.randn(2, 1024, 512, device=dev).to(torch.bfloat16)
+    g = torch.randn(2, 1024, 512, device=dev)
+
+    def run(pair):
+        dec.zero_grad()
+        s, f = s0.clone().requires_grad_(True), f0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = dec.forward_tokens((s, f) if pair else s + f)
+        y.float().backward(g)
+        return [y.detach(), s.grad, f.grad] + [p.grad.clone() for p in dec.parameters()]
+
+    for x, y in zip(run(True), run(False)):
+        assert torch.equal(x, y)
