@@ -301,12 +301,13 @@ int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *
                                void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_blend_fwd / pcops_blend_bwd: PointSea's path selection out = s * a + (1 - s) * b over n
  *   elements (n % 8 == 0; models_PointSea/PointSea.py:128-131), s `score_dtype` (0 fp32, 1 bf16), a, b,
- *   out, g, da, db fp32, dscore in s's dtype.  torch's per-op roundings: for a bf16 s, 1 - s is rounded
- *   to bf16 and dscore = bf16(bf16(g * a) - bf16(g * b)).  da / db / dscore may be NULL (not needed). */
-int pcops_blend_fwd(const void *score, int score_dtype, const float *a, const float *b, long long n, float *out,
-                    pcops_stream_t stream);
-int pcops_blend_bwd(const float *g, const void *score, int score_dtype, const float *a, const float *b, long long n,
-                    float *da, float *db, void *dscore, pcops_stream_t stream);
+ *   da, db fp32, out `out_dtype` (bf16: the value autocast hands the next GEMM), g `g_dtype`, dscore in
+ *   s's dtype.  torch's per-op roundings: for a bf16 s, 1 - s is rounded to bf16 and
+ *   dscore = bf16(bf16(g * a) - bf16(g * b)).  da / db / dscore may be NULL (not needed). */
+int pcops_blend_fwd(const void *score, int score_dtype, const float *a, const float *b, long long n, void *out,
+                    int out_dtype, pcops_stream_t stream);
+int pcops_blend_bwd(const void *g, int g_dtype, const void *score, int score_dtype, const float *a, const float *b,
+                    long long n, float *da, float *db, void *dscore, pcops_stream_t stream);
 /* pcops_layernorm_bwd_bf16g: pcops_layernorm_bwd(_colsum) with BOTH upstream gradients bf16:
  *   dy = dy_a + dy16, dy_a the gradient of the fp32 output y32 as a bf16 consumer produced it
  *   (the block sum bf16(y32 + f): replaces widening it to fp32 in a separate pass; the sum is

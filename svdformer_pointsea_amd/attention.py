@@ -784,32 +784,37 @@ class _Blend(Function):
     the four-op expression (score bf16 under autocast, a / b the fp32 residual streams)."""
 
     @staticmethod
-    def forward(ctx, score, a, b):
-        out = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+    def forward(ctx, score, a, b, out_dtype):
+        out = torch.empty(a.shape, dtype=out_dtype, device=a.device)
         with torch.cuda.device(a.device):
             call("blend", lib().pcops_blend_fwd, ptr(score), _dt(score), ptr(a), ptr(b), a.numel(), ptr(out),
-                 stream_of(a))
+                 _DT[out_dtype], stream_of(a))
         ctx.save_for_backward(score, a, b)
         return out
 
     @staticmethod
     def backward(ctx, g):
         score, a, b = ctx.saved_tensors
-        g = g.contiguous().float()
+        g = g.contiguous()
+        if g.dtype not in _DT:
+            g = g.float()
         ds = torch.empty_like(score) if ctx.needs_input_grad[0] else None
         da = torch.empty_like(a) if ctx.needs_input_grad[1] else None
         db = torch.empty_like(b) if ctx.needs_input_grad[2] else None
         with torch.cuda.device(g.device):
-            call("blend_bwd", lib().pcops_blend_bwd, ptr(g), ptr(score), _dt(score), ptr(a), ptr(b), g.numel(),
-                 ptr(da), ptr(db), ptr(ds), stream_of(g))
-        return ds, da, db
+            call("blend_bwd", lib().pcops_blend_bwd, ptr(g), _dt(g), ptr(score), _dt(score), ptr(a), ptr(b),
+                 g.numel(), ptr(da), ptr(db), ptr(ds), stream_of(g))
+        return ds, da, db, None
 
 
-def blend(score, a, b):
-    """score * a + (1 - score) * b (PointSea's SDG path selection)."""
+def blend(score, a, b, gemm_only=False):
+    """score * a + (1 - score) * b (PointSea's SDG path selection).  gemm_only: the result feeds only a
+    GEMM, so under bf16 autocast it is produced as the bf16 operand the cast would make (its gradient
+    arrives as the GEMM's bf16 input gradient, the value the widening cast would have carried)."""
     if (_PCOPS_BLEND and score.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32
             and score.dtype in _DT and score.shape == a.shape == b.shape and a.numel() % 8 == 0):
-        return _Blend.apply(score.contiguous(), a.contiguous(), b.contiguous())
+        odt = torch.bfloat16 if (gemm_only and _want_bf16()) else torch.float32
+        return _Blend.apply(score.contiguous(), a.contiguous(), b.contiguous(), odt)
     return score * a + (1 - score) * b
 
 

@@ -413,9 +413,9 @@ __device__ __forceinline__ float blend_t2(float s) {
   return ST == 1 ? (float)(__bf16)t : t;
 }
 
-template <int ST>
+template <int ST, int OT>
 __global__ __launch_bounds__(256) void blend_fwd_kernel(const void *__restrict__ score, const float *__restrict__ a,
-                                                        const float *__restrict__ b, float *__restrict__ out,
+                                                        const float *__restrict__ b, void *__restrict__ out,
                                                         long long n8) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
     V8 sv, av, bv, o;
@@ -428,18 +428,21 @@ __global__ __launch_bounds__(256) void blend_fwd_kernel(const void *__restrict__
       const float t3 = blend_t2<ST>(sv.v[k]) * bv.v[k];
       o.v[k] = t1 + t3;
     }
-    st8_f32(out, 8 * i, o);
+    if constexpr (OT == 0)
+      st8_f32(reinterpret_cast<float *>(out), 8 * i, o);
+    else
+      st8_bf16(reinterpret_cast<__bf16 *>(out), 8 * i, o);  // the GEMM operand autocast would cast it to
   }
 }
 
-template <int ST>
-__global__ __launch_bounds__(256) void blend_bwd_kernel(const float *__restrict__ g, const void *__restrict__ score,
+template <int ST, int GT>
+__global__ __launch_bounds__(256) void blend_bwd_kernel(const void *__restrict__ g, const void *__restrict__ score,
                                                         const float *__restrict__ a, const float *__restrict__ b,
                                                         float *__restrict__ da, float *__restrict__ db,
                                                         void *__restrict__ ds, long long n8) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
     V8 gv, sv, av, bv, oa, ob, os;
-    ld8c<0>(gv, g, 8 * i);
+    ld8c<GT>(gv, g, 8 * i);
     ld8c<ST>(sv, score, 8 * i);
     ld8c<0>(av, a, 8 * i);
     ld8c<0>(bv, b, 8 * i);
@@ -938,35 +941,40 @@ unsigned blend_grid(long long n8) {
 }  // namespace
 
 extern "C" int pcops_blend_fwd(const void *score, int score_dtype, const float *a, const float *b, long long n,
-                               float *out, pcops_stream_t stream) {
-  if (n < 0 || !dt_ok(score_dtype)) return PCOPS_ERR_INVALID;
+                               void *out, int out_dtype, pcops_stream_t stream) {
+  if (n < 0 || !dt_ok(score_dtype) || !dt_ok(out_dtype)) return PCOPS_ERR_INVALID;
   if (n == 0) return PCOPS_OK;
   if (!score || !a || !b || !out) return PCOPS_ERR_INVALID;
   if (n % 8) return PCOPS_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const long long n8 = n / 8;
-  if (score_dtype == 1)
-    hipLaunchKernelGGL((blend_fwd_kernel<1>), dim3(blend_grid(n8)), dim3(256), 0, s, score, a, b, out, n8);
-  else
-    hipLaunchKernelGGL((blend_fwd_kernel<0>), dim3(blend_grid(n8)), dim3(256), 0, s, score, a, b, out, n8);
+  const dim3 grid(blend_grid(n8));
+  switch (score_dtype * 2 + out_dtype) {
+    case 0: hipLaunchKernelGGL((blend_fwd_kernel<0, 0>), grid, dim3(256), 0, s, score, a, b, out, n8); break;
+    case 1: hipLaunchKernelGGL((blend_fwd_kernel<0, 1>), grid, dim3(256), 0, s, score, a, b, out, n8); break;
+    case 2: hipLaunchKernelGGL((blend_fwd_kernel<1, 0>), grid, dim3(256), 0, s, score, a, b, out, n8); break;
+    default: hipLaunchKernelGGL((blend_fwd_kernel<1, 1>), grid, dim3(256), 0, s, score, a, b, out, n8); break;
+  }
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
 
-extern "C" int pcops_blend_bwd(const float *g, const void *score, int score_dtype, const float *a, const float *b,
-                               long long n, float *da, float *db, void *dscore, pcops_stream_t stream) {
-  if (n < 0 || !dt_ok(score_dtype)) return PCOPS_ERR_INVALID;
+extern "C" int pcops_blend_bwd(const void *g, int g_dtype, const void *score, int score_dtype, const float *a,
+                               const float *b, long long n, float *da, float *db, void *dscore,
+                               pcops_stream_t stream) {
+  if (n < 0 || !dt_ok(score_dtype) || !dt_ok(g_dtype)) return PCOPS_ERR_INVALID;
   if (n == 0) return PCOPS_OK;
   if (!g || !score || !a || !b) return PCOPS_ERR_INVALID;
   if (n % 8) return PCOPS_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const long long n8 = n / 8;
-  if (score_dtype == 1)
-    hipLaunchKernelGGL((blend_bwd_kernel<1>), dim3(blend_grid(n8)), dim3(256), 0, s, g, score, a, b, da, db, dscore,
-                       n8);
-  else
-    hipLaunchKernelGGL((blend_bwd_kernel<0>), dim3(blend_grid(n8)), dim3(256), 0, s, g, score, a, b, da, db, dscore,
-                       n8);
+  const dim3 grid(blend_grid(n8));
+  switch (score_dtype * 2 + g_dtype) {
+    case 0: hipLaunchKernelGGL((blend_bwd_kernel<0, 0>), grid, dim3(256), 0, s, g, score, a, b, da, db, dscore, n8); break;
+    case 1: hipLaunchKernelGGL((blend_bwd_kernel<0, 1>), grid, dim3(256), 0, s, g, score, a, b, da, db, dscore, n8); break;
+    case 2: hipLaunchKernelGGL((blend_bwd_kernel<1, 0>), grid, dim3(256), 0, s, g, score, a, b, da, db, dscore, n8); break;
+    default: hipLaunchKernelGGL((blend_bwd_kernel<1, 1>), grid, dim3(256), 0, s, g, score, a, b, da, db, dscore, n8); break;
+  }
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

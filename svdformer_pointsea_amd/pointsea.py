@@ -129,7 +129,7 @@ class SDG(nn.Module):
             parts.append(F_L_prev.to(parts[0].dtype))
         parts += [f_g_current.expand(B, N, -1).to(parts[0].dtype), g.expand(B, N, -1).to(parts[0].dtype)]
         score = torch.sigmoid(_lin(self.fusionMlp.mlp[0], torch.cat(parts, dim=-1)))
-        F_L = blend(score, F_Q_, F_H_)                     # score * F_Q_ + (1 - score) * F_H_
+        F_L = blend(score, F_Q_, F_H_, gemm_only=True)     # score * F_Q_ + (1 - score) * F_H_; read by conv_ps only
         # conv_ps(F_L).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n
         T = _lin(self.conv_ps, F_L)
         r = self.ratio

@@ -1051,3 +1051,27 @@ def test_pointsea_decoder_pair_input_bitwise(dev, monkeypatch):
 
     for x, y in zip(run(True), run(False)):
         assert torch.equal(x, y)
+
+
+def test_blend_gemm_operand_bitwise(dev, monkeypatch):
+    """blend(..., gemm_only=True) under bf16 autocast emits the bf16 GEMM operand directly and takes
+    the GEMM's bf16 input gradient: same output and gradients as the fp32 blend followed by the cast."""
+    import svdformer_pointsea_amd.attention as A
+
+    torch.manual_seed(11)
+    shape = (4, 512, 256)
+    s0 = torch.sigmoid(torch.randn(shape, device=dev)).to(torch.bfloat16)
+    a0, b0 = torch.randn(shape, device=dev), torch.randn(shape, device=dev)
+    g = torch.randn(shape, device=dev).to(torch.bfloat16)
+
+    def run(direct):
+        s, a, b = (t.clone().requires_grad_(True) for t in (s0, a0, b0))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = A.blend(s, a, b, gemm_only=True) if direct else A.blend(s, a, b).to(torch.bfloat16)
+        out.backward(g)
+        return out.detach(), s.grad, a.grad, b.grad
+
+    got, ref = run(True), run(False)
+    assert got[0].dtype == torch.bfloat16
+    for x, y in zip(got, ref):
+        assert torch.equal(x, y)
