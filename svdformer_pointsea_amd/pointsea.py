@@ -23,16 +23,23 @@ Reference map:
   Model                                 PointSea.py:250-272
   SDG_Decoder / self_attention_woinp    models_PointSea/model_utils.py:463-509
 """
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import PosEmbedding, SDG_Decoder_PointSea, blend, cross_attention, self_attention, to_tokens
+from .attention import (PosEmbedding, SDG_Decoder_PointSea, _want_bf16, blend, block_sum, cross_attention,
+                        self_attention, to_tokens)
 from .chamfer3D import chamfer_3DDist
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act
 from .pointnet2_utils import furthest_point_sample, gather_operation
 from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin
+
+
+# PCOPS_PS_CAT16=0: the path-selection concatenation in fp32, cast by autocast (A/B)
+_CAT16 = os.environ.get("PCOPS_PS_CAT16", "1") != "0"
 
 
 # ----------------------------------------------------------------- image encoder
@@ -124,10 +131,18 @@ class SDG(nn.Module):
         s, f = self.cross1.forward_tokens(F_Q, local)
         F_H_ = self.decoder2.forward_tokens((s, f))        # its first op is a LayerNorm of s + f
         # path selection
-        parts = [F_Q_ + F_H_]
-        if self.with_prev:
-            parts.append(F_L_prev.to(parts[0].dtype))
-        parts += [f_g_current.expand(B, N, -1).to(parts[0].dtype), g.expand(B, N, -1).to(parts[0].dtype)]
+        if _CAT16 and F_Q_.is_cuda and _want_bf16():
+            # the concatenation only feeds fusionMlp's GEMM: built from parts already in the bf16
+            # operand dtype (cat of bf16 parts == bf16 of the fp32 cat), the sum rounded once in its add
+            parts = [block_sum(F_Q_, F_H_)]
+            if self.with_prev:
+                parts.append(F_L_prev.to(torch.bfloat16))
+            parts += [f_g_current.expand(B, N, -1).to(torch.bfloat16), g.expand(B, N, -1).to(torch.bfloat16)]
+        else:
+            parts = [F_Q_ + F_H_]
+            if self.with_prev:
+                parts.append(F_L_prev.to(parts[0].dtype))
+            parts += [f_g_current.expand(B, N, -1).to(parts[0].dtype), g.expand(B, N, -1).to(parts[0].dtype)]
         score = torch.sigmoid(_lin(self.fusionMlp.mlp[0], torch.cat(parts, dim=-1)))
         F_L = blend(score, F_Q_, F_H_, gemm_only=True)     # score * F_Q_ + (1 - score) * F_H_; read by conv_ps only
         # conv_ps(F_L).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n

@@ -106,3 +106,37 @@ def test_seprate_point_cloud_without_crop_same_input(dev):
         a, _ = seprate_point_cloud(gt, n, k, generator=torch.Generator(device=dev).manual_seed(8))
         b, cb = seprate_point_cloud(gt, n, k, generator=torch.Generator(device=dev).manual_seed(8), want_crop=False)
         assert cb is None and torch.equal(a, b)
+
+
+def test_pointsea_glue_fusions_match_unfused(dev, monkeypatch):
+    """The PointSea SDG glue fusions (path-selection blend in one launch emitting the bf16 conv_ps
+    operand; the selection concatenation from bf16 parts) against the plain torch expressions, one
+    bf16-autocast forward + backward of the model: outputs and every parameter gradient bitwise,
+    except that the broadcast f_g_current part's gradient is summed over a differently laid-out
+    tensor (reduction order) -- those gradients within 1e-5 relative."""
+    import svdformer_pointsea_amd.attention as A
+    import svdformer_pointsea_amd.pointsea as PS
+
+    torch.manual_seed(2)
+    model = Model(Config55).cuda()
+    partial, gt = synth_55(2, 7, "cuda")
+    render = PCViews_Real(TRANS=-Config55.NETWORK.view_distance)
+    depth = render.get_img(partial)
+
+    def run(fused):
+        monkeypatch.setattr(A, "_PCOPS_BLEND", fused)
+        monkeypatch.setattr(PS, "_CAT16", fused)
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            pcds = model(partial, depth)
+            loss, _ = get_loss_PM(pcds, partial, gt, sqrt=False)
+        loss.backward()
+        return [p.detach().clone() for p in pcds], {n: p.grad.clone() for n, p in model.named_parameters()
+                                                     if p.grad is not None}
+
+    (out_a, g_a), (out_b, g_b) = run(True), run(False)
+    for x, y in zip(out_a, out_b):
+        assert torch.equal(x, y)
+    assert g_a.keys() == g_b.keys()
+    for n in g_a:
+        torch.testing.assert_close(g_a[n], g_b[n], rtol=1e-5, atol=1e-7, msg=n)
