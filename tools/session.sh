@@ -1,14 +1,9 @@
 set -o pipefail
-O=gpurun_out/r4t; mkdir -p $O
+O=gpurun_out/r4v; mkdir -p $O
 export TMPDIR=/tmp
-run() {  # tag, env...
-  local tag=$1; shift
-  env "$@" timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$tag -o run -- \
-    python tools/knn_bench.py > $O/knn_$tag.txt 2>&1 || return 1
-  f=$(find $O/prof_$tag -name '*kernel_stats.csv' -print -quit); cp "$f" $O/stats_$tag.csv
-  find $O/prof_$tag -name '*kernel_trace.csv' -delete
-}
-run full PCOPS_KNN_SHARE=1 || exit 1
-run noshare PCOPS_KNN_SHARE=0 || exit 1
-run abl1 PCOPS_LIB_PATH=$PWD/abl/knn1/libpcops.so || exit 1
-run abl2 PCOPS_LIB_PATH=$PWD/abl/knn2/libpcops.so || exit 1
+export PYTEST_K="blend or pair_input or pointsea or models_golden"
+bash tools/gpu_run.sh $O tests_k || exit 1
+for i in 1 2; do
+  timeout -k 10 300 python bench.py --model pointsea --no-cpu-baseline > $O/ps_new_$i.json 2> $O/ps_new_$i.err || exit 1
+  PCOPS_BLEND=0 timeout -k 10 300 python bench.py --model pointsea --no-cpu-baseline > $O/ps_noblend_$i.json 2> $O/ps_noblend_$i.err || exit 1
+done
