@@ -248,6 +248,12 @@ def kernel_work(name, a):
         return float(2 * 2 * a[2] * a[3] * a[4] * a[5]), "GB/s", HBM_PEAK, "hbm"
     if name == "add":            # a, adt, b, bdt, out, odt, n
         return float(a[6] * (es(a[1]) + es(a[3]) + es(a[5]))), "GB/s", HBM_PEAK, "hbm"
+    if name == "blend":          # score, sdt, a, b, n, out, odt: read score + two fp32 streams, write out
+        return float(a[4] * (es(a[1]) + 8 + es(a[6]))), "GB/s", HBM_PEAK, "hbm"
+    if name == "blend_bwd":      # g, gdt, score, sdt, a, b, n, da, db, ds: read g, score, a, b; write da, db, ds
+        return float(a[6] * (es(a[1]) + 2 * es(a[3]) + 16)), "GB/s", HBM_PEAK, "hbm"
+    if name == "add_posemb":     # a, adt, cd, div, B, N, H, out, odt: read a + cd, write out
+        return float(a[4] * a[5] * (a[6] * (es(a[1]) + es(a[8])) + 4)), "GB/s", HBM_PEAK, "hbm"
     if name == "max_k":          # x, dt, rows, K, C, out, arg: read K rows, write the max + a uint8 argmax
         return float(a[2] * a[4] * ((a[3] + 1) * es(a[1]) + 1)), "GB/s", HBM_PEAK, "hbm"
     if name == "max_k_grad":     # g, dt, arg, rows, K, C, gx: read g + argmax, write the K rows
@@ -293,6 +299,7 @@ _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_d
             "conv3x3_fwd": r"conv3x3_fwd_kernel", "conv3x3_dgrad": r"conv3x3_fwd_kernel",
             "conv3x3_wgrad": (r"conv3x3_wgrad_kernel|conv3x3_wgrad_reduce", r"conv3x3_wgrad_kernel"),
             "add": r"add_kernel", "max_k": r"max_k_kernel", "max_k_grad": r"max_k_grad_kernel",
+            "blend": r"blend_fwd_kernel", "blend_bwd": r"blend_bwd_kernel", "add_posemb": r"add_posemb_kernel",
             "gelu_bwd": (r"gelu_bwd_partial_kernel|colsum_final", r"gelu_bwd_partial_kernel"),
             "edge_group": r"edge_group_kernel",
             "edge_group_grad": (r"edge_group_grad_own_kernel|edge_group_grad_scatter_kernel",
