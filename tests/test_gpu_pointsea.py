@@ -134,6 +134,12 @@ def test_pointsea_glue_fusions_match_unfused(dev, monkeypatch):
         return [p.detach().clone() for p in pcds], {n: p.grad.clone() for n, p in model.named_parameters()
                                                      if p.grad is not None}
 
+    # the first call of a conv shape may run a different MIOpen algorithm than later calls (the
+    # image encoder's output moved in bf16 between two otherwise identical first passes): warm up
+    # once and pin deterministic algorithms, so the comparison sees only the fusions
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
+    run(False)
     (out_a, g_a), (out_b, g_b) = run(True), run(False)
     for x, y in zip(out_a, out_b):
         assert torch.equal(x, y)
