@@ -248,6 +248,10 @@ def kernel_work(name, a):
         return float(2 * 2 * a[2] * a[3] * a[4] * a[5]), "GB/s", HBM_PEAK, "hbm"
     if name == "add":            # a, adt, b, bdt, out, odt, n
         return float(a[6] * (es(a[1]) + es(a[3]) + es(a[5]))), "GB/s", HBM_PEAK, "hbm"
+    if name == "adam_flat":      # param, g16, g32, n16, n, m, v, shadow, ...: read g + p, m, v; write p, m, v (+ shadow)
+        n16 = a[3] if a[1] else 0
+        sh = a[3] if a[7] else 0
+        return float(a[4] * 28 - n16 * 2 + sh * 2), "GB/s", HBM_PEAK, "hbm"
     if name == "blend":          # score, sdt, a, b, n, out, odt: read score + two fp32 streams, write out
         return float(a[4] * (es(a[1]) + 8 + es(a[6]))), "GB/s", HBM_PEAK, "hbm"
     if name == "blend_bwd":      # g, gdt, score, sdt, a, b, n, da, db, ds: read g, score, a, b; write da, db, ds
@@ -300,6 +304,7 @@ _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_d
             "conv3x3_wgrad": (r"conv3x3_wgrad_kernel|conv3x3_wgrad_reduce", r"conv3x3_wgrad_kernel"),
             "add": r"add_kernel", "max_k": r"max_k_kernel", "max_k_grad": r"max_k_grad_kernel",
             "blend": r"blend_fwd_kernel", "blend_bwd": r"blend_bwd_kernel", "add_posemb": r"add_posemb_kernel",
+            "adam_flat": r"adam_flat_kernel",
             "gelu_bwd": (r"gelu_bwd_partial_kernel|colsum_final", r"gelu_bwd_partial_kernel"),
             "edge_group": r"edge_group_kernel",
             "edge_group_grad": (r"edge_group_grad_own_kernel|edge_group_grad_scatter_kernel",
@@ -656,7 +661,7 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
     the timed replays; a non-finite loss anywhere -- warm-up, timed replays or
     the eager timing steps -- fails the run."""
     from svdformer_pointsea_amd import _lib
-    from svdformer_pointsea_amd.train import BucketedAllReduce, FlatParams, TrainSchedule
+    from svdformer_pointsea_amd.train import BucketedAllReduce, FlatAdam, FlatParams, TrainSchedule
 
     L = Leg()
     torch.manual_seed(0)  # identical init on every rank
@@ -671,6 +676,12 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
     # the schedule writes each step (warm-up per batch, train_pcn.py:132-134)
     opt = wl.optimizer([fp.master()], lr=torch.tensor(1e-4, device=device) if use_graph else 1e-4, fused=True,
                        capturable=use_graph)
+    # the update itself on libpcops (train.FlatAdam): reads the bf16 gradient bucket, writes the bf16
+    # shadows, keeps torch's optimizer state; PCOPS_FLAT_ADAM=0 runs torch's fused Adam (A/B)
+    fopt = (FlatAdam(opt, fp) if fp.shadow and os.environ.get("PCOPS_FLAT_ADAM", "1") != "0" else None)
+    L.optimizer_impl = "libpcops pcops_adam_flat" if fopt is not None else "torch fused Adam"
+    if fopt is not None:
+        fp.refresh()   # the first step's shadows; afterwards every update writes them
     schedule = TrainSchedule(opt, wl.name)
     partial, gt = wl.synth(batch, 1000 + rank, device)
     L.partial, L.gt = partial, gt
@@ -692,7 +703,8 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
 
     def fwd_bwd():
         fp.zero_grad()
-        fp.refresh()
+        if fopt is None:
+            fp.refresh()
         # the loss's gt FPS chain depends on gt only: it runs on a second
         # stream beside the whole forward pass (FPS occupies B CUs)
         with _lib.fork(device, lane=1, inputs=(gt,)) as br:
@@ -711,7 +723,7 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
         if sync[0] is not None:
             sync[0].finish()   # the bucketed all-reduces were issued during backward
         else:
-            fp.collect()
+            fp.collect(widen=fopt is None or use_dist)
         if prefetch:
             staged[0].copy_(bn.join(nxt))
         loss_acc.add_(loss.detach())  # logged without a host sync
@@ -720,10 +732,16 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
         if use_dist and sync[0] is None:
             fp.allreduce(world)
 
+    def opt_step():
+        if fopt is not None:
+            fopt.step(bf16_grads=not use_dist)
+        else:
+            opt.step()
+
     def eager_step():
         fwd_bwd()
         grad_sync()
-        opt.step()
+        opt_step()
         schedule.batch_end()
 
     def check_finite(what):
@@ -785,7 +803,7 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
                 with torch.cuda.graph(g_fb):
                     fwd_bwd()
         with torch.cuda.graph(g_opt):
-            opt.step()
+            opt_step()
 
         def step():
             g_fb.replay()
@@ -882,7 +900,7 @@ def extra_leg(args, name, batch, amp, device, steps):
                     name + ("" if amp else "-fp32"))
     out = {"workload": wl.desc, "batch": batch, "dtype": "bf16" if amp else "f32", "steps": steps,
            "ms_per_step": round(leg.ms_per_step, 3), "samples_per_s": round(batch * 1e3 / leg.ms_per_step, 2),
-           "execution": "hip_graph" if leg.use_graph else "eager"}
+           "execution": "hip_graph" if leg.use_graph else "eager", "optimizer": leg.optimizer_impl}
     if name == "pointsea" and amp:
         out["input_prefetch"] = not args.no_input_prefetch
     # the leg's own libpcops kernel table (HIP events of its eager timing steps)
@@ -937,6 +955,7 @@ def main():
     elapsed, spans, span_steps, sync = leg.elapsed, leg.spans, leg.span_steps, leg.sync
     use_graph, host_ms, nparams = leg.use_graph, leg.host * 1e3 / args.steps, leg.nparams
     idle_issue_ms = leg.idle_issue_ms
+    optimizer_impl = leg.optimizer_impl
 
     fp32_leg = None
     extra = {}
@@ -968,6 +987,7 @@ def main():
             "host_issue_ms_per_step": host_ms,
             "host_issue_idle_gpu_ms": None if idle_issue_ms is None else round(idle_issue_ms, 3),
             "execution": "hip_graph" if use_graph else "eager",
+            "optimizer": optimizer_impl,
             "grad_sync": ("none (single GPU)" if not use_dist else
                           f"bucketed all-reduce from backward hooks ({len(sync.buckets)} buckets of "
                           f"<= {args.bucket_mb:g} MB){' inside the captured graph' if use_graph else ''}"

@@ -299,6 +299,17 @@ int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *
                                int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
                                float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
                                void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+/* pcops_adam_flat: torch's Adam (adamw = 0; weight decay added to the gradient) or AdamW (adamw = 1;
+ *   decoupled decay) over n fp32 master weights `param` with its exp_avg / exp_avg_sq state
+ *   (core/train_pcn.py:57-60, core/train_55.py:86-88): gradients [0, n16) from grad16 (bf16) when
+ *   given, everything else from grad32; the new weights of [0, n16) also written to shadow16 (bf16)
+ *   when given.  step_dev: the step count AFTER this update (device fp32 scalar, incremented by the
+ *   caller); lr_dev: a device fp32 learning rate (NULL: `lr`).  Replaces optimizer.step() with the
+ *   gradient widening and the bf16 weight refresh around it. */
+int pcops_adam_flat(float *param, const void *grad16, const float *grad32, long long n16, long long n,
+                    float *exp_avg, float *exp_avg_sq, void *shadow16, const float *lr_dev, float lr,
+                    const float *step_dev, float beta1, float beta2, float eps, float weight_decay, int adamw,
+                    pcops_stream_t stream);
 /* pcops_blend_fwd / pcops_blend_bwd: PointSea's path selection out = s * a + (1 - s) * b over n
  *   elements (n % 8 == 0; models_PointSea/PointSea.py:128-131), s `score_dtype` (0 fp32, 1 bf16), a, b,
  *   da, db fp32, out `out_dtype` (bf16: the value autocast hands the next GEMM), g `g_dtype`, dscore in

@@ -152,14 +152,17 @@ class FlatParams:
             g = h
         return g.as_strided((g.numel(),), (1,), g.storage_offset())
 
-    def collect(self):
+    def collect(self, widen=True):
         """fp32 gradient bucket <- the shadows' bf16 gradients (zeros where a
-        shadow received none): one batched concatenation, one cast kernel."""
+        shadow received none): one batched concatenation, one cast kernel.
+        widen=False leaves the shadow region in the bf16 bucket (grad16) for an
+        optimizer that reads it there (FlatAdam); the fp32 region is gathered."""
         if not self._order:
             return
         with torch.no_grad():
             if _GRADS == "preset":
-                self.grad[:self.n16].copy_(self.grad16)
+                if widen:
+                    self.grad[:self.n16].copy_(self.grad16)
                 return
             parts = []
             for w in self._order:
@@ -167,7 +170,8 @@ class FlatParams:
                 parts.append(torch.zeros(w.numel(), dtype=self.grad16.dtype, device=self.grad16.device)
                              if g is None else self._physical(g, w))
             torch.cat(parts, out=self.grad16)
-            self.grad[:self.n16].copy_(self.grad16)
+            if widen:
+                self.grad[:self.n16].copy_(self.grad16)
             self._collect32(self.n16, self.n_train, self._order32)
 
     def _collect32(self, lo, hi, entries, stream=None):
@@ -193,6 +197,50 @@ class FlatParams:
             import torch.distributed as dist
             dist.all_reduce(self.grad)
             self.grad.mul_(1.0 / world)
+
+
+class FlatAdam:
+    """`step()` of a torch Adam / AdamW over FlatParams.master() on libpcops (pcops_adam_flat): one
+    pass that reads the shadow region's gradients from the bf16 bucket (collect(widen=False)), the
+    rest from the fp32 bucket, updates master / exp_avg / exp_avg_sq in the torch optimizer's own
+    state (so its state_dict, checkpoints and LR schedule are unchanged) and writes the new bf16
+    shadow weights -- replacing the widening cast, torch's fused update and the shadow refresh.
+    Arithmetic: torch's Adam (core/train_pcn.py:57-60 Adam, core/train_55.py:86-88 AdamW), the
+    device step tensor incremented first as in torch's capturable path."""
+
+    def __init__(self, opt, fp):
+        if len(opt.param_groups) != 1 or len(opt.param_groups[0]["params"]) != 1:
+            raise ValueError("FlatAdam: one param group holding FlatParams.master()")
+        g = opt.param_groups[0]
+        if g.get("amsgrad") or g.get("maximize") or g.get("differentiable"):
+            raise ValueError("FlatAdam: amsgrad / maximize / differentiable are not used by the reference")
+        self.opt, self.fp = opt, fp
+        self.p = g["params"][0]
+        self.adamw = isinstance(opt, torch.optim.AdamW)
+
+    @torch.no_grad()
+    def step(self, bf16_grads=True):
+        """bf16_grads: the shadow region's gradients are in fp.grad16 (collect(widen=False));
+        False: the whole fp32 bucket (the data-parallel path's all-reduced gradients)."""
+        from ._lib import call, lib, ptr, stream_of
+
+        g = self.opt.param_groups[0]
+        p = self.p
+        st = self.opt.state[p]
+        if not st:
+            st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        st["step"].add_(1)
+        lr = g["lr"]
+        lr_dev = lr if isinstance(lr, torch.Tensor) else None
+        fp = self.fp
+        beta1, beta2 = g["betas"]
+        with torch.cuda.device(p.device):
+            call("adam_flat", lib().pcops_adam_flat, ptr(p), ptr(fp.grad16) if bf16_grads else None, ptr(fp.grad),
+                 fp.n16, p.numel(), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), ptr(fp.flat16),
+                 ptr(lr_dev), float(lr) if lr_dev is None else 0.0, ptr(st["step"]), float(beta1), float(beta2),
+                 float(g["eps"]), float(g["weight_decay"]), int(self.adamw), stream_of(p))
 
 
 class BucketedAllReduce:

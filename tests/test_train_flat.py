@@ -333,3 +333,58 @@ def test_checkpoint_roundtrip_capturable_flat_optimizer_gpu():
         o.step()
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         assert torch.equal(pa.data, pb.data), n
+
+
+class _NetMix(nn.Module):
+    """Linear layers (bf16 shadows) around a LayerNorm (fp32 region), sizes not multiples of 4."""
+
+    def __init__(self):
+        super().__init__()
+        self.l1 = nn.Linear(37, 129)
+        self.norm = nn.LayerNorm(129)
+        self.l2 = nn.Linear(129, 19)
+
+    def forward(self, x):
+        return self.l2(self.norm(self.l1(x)).relu()).square().mean()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["adam", "adamw"])
+def test_flat_adam_matches_torch_fused(kind):
+    """train.FlatAdam (pcops_adam_flat: bf16 shadow-region gradients read from the bf16 bucket, the new
+    shadows written by the update) against torch's fused capturable Adam / AdamW on the same flat
+    buffers: master weights and both moments within fp32 rounding of torch's (the kernel's
+    arithmetic order is torch's; torch forms some products in double), shadows = bf16(master), the
+    torch optimizer's state_dict layout unchanged."""
+    from svdformer_pointsea_amd.train import FlatAdam
+
+    dev = "cuda"
+    torch.manual_seed(4)
+    a = _NetMix().to(dev)
+    b = copy.deepcopy(a)
+    fa, fb = FlatParams(a, dev), FlatParams(b, dev)
+    mk = (lambda ps, lr: torch.optim.Adam(ps, lr=lr, betas=(0.9, 0.999), weight_decay=0, fused=True,
+                                          capturable=True)) if kind == "adam" else \
+         (lambda ps, lr: torch.optim.AdamW(ps, lr=lr, weight_decay=5e-4, fused=True, capturable=True))
+    oa = mk([fa.master()], torch.tensor(1e-3, device=dev))
+    ob = mk([fb.master()], torch.tensor(1e-3, device=dev))
+    flat = FlatAdam(ob, fb)
+    fb.refresh()
+    for step in range(5):
+        x = torch.randn(64, 37, generator=torch.Generator().manual_seed(step)).to(dev)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            fa.zero_grad()
+            fa.refresh()
+            fa.forward(x).backward()
+            fb.zero_grad()
+            fb.forward(x).backward()
+        fa.collect()
+        fb.collect(widen=False)
+        oa.step()
+        flat.step()
+        torch.testing.assert_close(fb.flat, fa.flat, rtol=2e-6, atol=1e-8)
+    (sa,), (sb,) = oa.state.values(), ob.state.values()
+    assert sorted(sa) == sorted(sb) and torch.equal(sa["step"], sb["step"])
+    torch.testing.assert_close(sb["exp_avg"], sa["exp_avg"], rtol=2e-6, atol=1e-10)
+    torch.testing.assert_close(sb["exp_avg_sq"], sa["exp_avg_sq"], rtol=2e-6, atol=1e-14)
+    assert torch.equal(fb.flat16, fb.flat[:fb.n16].to(torch.bfloat16))
