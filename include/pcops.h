@@ -304,11 +304,12 @@ int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *
  *   (core/train_pcn.py:57-60, core/train_55.py:86-88): gradients [0, n16) from grad16 (bf16) when
  *   given, everything else from grad32; the new weights of [0, n16) also written to shadow16 (bf16)
  *   when given.  step_dev: the step count AFTER this update (device fp32 scalar, incremented by the
- *   caller); lr_dev: a device fp32 learning rate (NULL: `lr`).  Replaces optimizer.step() with the
- *   gradient widening and the bf16 weight refresh around it. */
+ *   caller); lr_dev: a device fp32 learning rate (NULL: `lr`).  Hyper-parameters are doubles and
+ *   enter the arithmetic as torch's fused Adam has them (products with them formed in double).
+ *   Replaces optimizer.step() with the gradient widening and the bf16 weight refresh around it. */
 int pcops_adam_flat(float *param, const void *grad16, const float *grad32, long long n16, long long n,
-                    float *exp_avg, float *exp_avg_sq, void *shadow16, const float *lr_dev, float lr,
-                    const float *step_dev, float beta1, float beta2, float eps, float weight_decay, int adamw,
+                    float *exp_avg, float *exp_avg_sq, void *shadow16, const float *lr_dev, double lr,
+                    const float *step_dev, double beta1, double beta2, double eps, double weight_decay, int adamw,
                     pcops_stream_t stream);
 /* pcops_blend_fwd / pcops_blend_bwd: PointSea's path selection out = s * a + (1 - s) * b over n
  *   elements (n % 8 == 0; models_PointSea/PointSea.py:128-131), s `score_dtype` (0 fp32, 1 bf16), a, b,

@@ -20,6 +20,7 @@ _lib = None
 P = ctypes.c_void_p
 I = ctypes.c_int
 F = ctypes.c_float
+D = ctypes.c_double
 LL = ctypes.c_longlong
 ULL = ctypes.c_ulonglong
 
@@ -72,7 +73,7 @@ _SIGS = {
     "pcops_layernorm_bwd_colsum_workspace_bytes": (ULL, [I, I]),
     "pcops_layernorm_bwd_colsum": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, I, P, ULL, P]),
     "pcops_layernorm_bwd_bf16g": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, I, P, ULL, P]),
-    "pcops_adam_flat": (I, [P, P, P, LL, LL, P, P, P, P, F, P, F, F, F, F, I, P]),
+    "pcops_adam_flat": (I, [P, P, P, LL, LL, P, P, P, P, D, P, D, D, D, D, I, P]),
     "pcops_blend_fwd": (I, [P, I, P, P, LL, P, I, P]),
     "pcops_blend_bwd": (I, [P, I, P, I, P, P, LL, P, P, P, P]),
     "pcops_sum_rows": (I, [P, I, LL, P, I, P]),

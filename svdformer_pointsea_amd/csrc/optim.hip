@@ -23,32 +23,33 @@ struct AdamArgs {
   __bf16 *shadow;
   long long n16, n;
   const float *lr_dev, *step_dev;
-  float lr, beta1, beta2, eps, wd;
+  double lr, beta1, beta2, eps, wd;
   int adamw;
 };
 
-__device__ __forceinline__ float adam_elem(const AdamArgs &a, float &p, float &m, float &v, float g, float step_size,
-                                           float bc2_sqrt, float lr) {
-  if (a.wd != 0.f) {
+// torch's fused Adam element update (ATen FusedAdamMathFunctor): the hyper-parameters are doubles,
+// so every product with one of them is formed in double and rounded once to fp32; the final
+// step_size * m / denom is fp32
+__device__ __forceinline__ void adam_elem(const AdamArgs &a, float &p, float &m, float &v, float g, float step_size,
+                                          float bc2_sqrt, double lr) {
+  if (a.wd != 0.0) {
     if (a.adamw)
-      p = p * (1.f - lr * a.wd);
+      p = (float)((double)p - lr * a.wd * (double)p);
     else
-      g = g + a.wd * p;
+      g = (float)((double)g + (double)p * a.wd);
   }
-  m = a.beta1 * m + (1.f - a.beta1) * g;
-  v = a.beta2 * v + (1.f - a.beta2) * g * g;
-  const float denom = sqrtf(v) / bc2_sqrt + a.eps;
+  m = (float)(a.beta1 * (double)m + (1.0 - a.beta1) * (double)g);
+  v = (float)(a.beta2 * (double)v + (1.0 - a.beta2) * (double)g * (double)g);
+  const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + a.eps);
   p = p - step_size * m / denom;
-  return p;
 }
 
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
-  const float t = *a.step_dev;
-  const float lr = a.lr_dev ? *a.lr_dev : a.lr;
-  // bias corrections in double, rounded once
-  const float bc1 = (float)(1.0 - pow((double)a.beta1, (double)t));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)a.beta2, (double)t));
-  const float step_size = lr / bc1;
+  const double t = *a.step_dev;
+  const double lr = a.lr_dev ? (double)*a.lr_dev : a.lr;
+  const float bc1 = (float)(1.0 - pow(a.beta1, t));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(a.beta2, t));
+  const float step_size = (float)(lr / (double)bc1);
   const long long stride = (long long)gridDim.x * 256 * 4;
   typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
   for (long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i0 < a.n; i0 += stride) {
@@ -96,8 +97,8 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
 }  // namespace
 
 extern "C" int pcops_adam_flat(float *param, const void *grad16, const float *grad32, long long n16, long long n,
-                               float *exp_avg, float *exp_avg_sq, void *shadow16, const float *lr_dev, float lr,
-                               const float *step_dev, float beta1, float beta2, float eps, float weight_decay,
+                               float *exp_avg, float *exp_avg_sq, void *shadow16, const float *lr_dev, double lr,
+                               const float *step_dev, double beta1, double beta2, double eps, double weight_decay,
                                int adamw, pcops_stream_t stream) {
   if (n < 0 || n16 < 0 || n16 > n) return PCOPS_ERR_INVALID;
   if (n == 0) return PCOPS_OK;
