@@ -1,4 +1,4 @@
 set -o pipefail
-O=gpurun_out/r4z; mkdir -p $O
+O=gpurun_out/r4t2; mkdir -p $O
 export TMPDIR=/tmp
-bash tools/gpu_run.sh $O tests smoke bench
+bash tools/gpu_run.sh $O trace pmc_traffic
