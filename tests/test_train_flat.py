@@ -349,10 +349,11 @@ class _NetMix(nn.Module):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["adam", "adamw"])
-def test_flat_adam_matches_torch_fused(kind):
+@pytest.mark.parametrize("kind,bf16_grads", [("adam", True), ("adamw", True), ("adam", False)])
+def test_flat_adam_matches_torch_fused(kind, bf16_grads):
     """train.FlatAdam (pcops_adam_flat: bf16 shadow-region gradients read from the bf16 bucket, the new
-    shadows written by the update) against torch's fused capturable Adam / AdamW on the same flat
+    shadows written by the update; bf16_grads=False: the whole fp32 bucket, the data-parallel path's)
+    against torch's fused capturable Adam / AdamW on the same flat
     buffers: master weights and both moments within fp32 rounding of torch's (the kernel's
     arithmetic order is torch's; torch forms some products in double), shadows = bf16(master), the
     torch optimizer's state_dict layout unchanged."""
@@ -379,9 +380,9 @@ def test_flat_adam_matches_torch_fused(kind):
             fb.zero_grad()
             fb.forward(x).backward()
         fa.collect()
-        fb.collect(widen=False)
+        fb.collect(widen=not bf16_grads)
         oa.step()
-        flat.step()
+        flat.step(bf16_grads=bf16_grads)
         torch.testing.assert_close(fb.flat, fa.flat, rtol=2e-6, atol=1e-8)
     (sa,), (sb,) = oa.state.values(), ob.state.values()
     assert sorted(sa) == sorted(sb) and torch.equal(sa["step"], sb["step"])
