@@ -1,4 +1,5 @@
 set -o pipefail
-O=gpurun_out/r4t2; mkdir -p $O
+O=gpurun_out/r4d1; mkdir -p $O
 export TMPDIR=/tmp
-bash tools/gpu_run.sh $O trace pmc_traffic
+export PYTEST_K="flat_adam or dist"
+bash tools/gpu_run.sh $O tests_k dist1
