@@ -35,12 +35,11 @@ from .chamfer3D import chamfer_3DDist
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act
 from .pointnet2_utils import furthest_point_sample, gather_operation
-from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin, _NoFork
+from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin
 
 
 # PCOPS_PS_CAT16=0: the path-selection concatenation in fp32, cast by autocast (A/B)
 _CAT16 = os.environ.get("PCOPS_PS_CAT16", "1") != "0"
-_POINT_STREAM = os.environ.get("PCOPS_PS_POINT_STREAM", "1") != "0"
 
 
 # ----------------------------------------------------------------- image encoder
@@ -186,14 +185,9 @@ class SVFNet(nn.Module):
 
     def forward(self, points, depth):
         B, _, N = points.size()
-        # the point branch (FPS + kNN grouping on B of 256 CUs, latency-bound) and the image branch
-        # (ResNet-18 over 3B views) are independent until viewattn1: the point branch on a stream
-        # of its own (PCOPS_PS_POINT_STREAM=0 runs them in order, A/B)
-        with (fork(points.device, lane=3, inputs=(points,)) if _POINT_STREAM else _NoFork()) as br:
-            f_p = self.point_feature_extractor(points)                 # (B, 256, 1)
         f_v = self.img_feature_extractor(depth.contiguous(memory_format=torch.channels_last))
         f_v = f_v.flatten(2)                                           # 'bv c h w -> bv c (h w)'
-        f_p = br.join(f_p)
+        f_p = self.point_feature_extractor(points)                     # (B, 256, 1)
         view_feature_1 = self.posmlp(self.view_point.expand(B, 3, 3))  # (B, 256, 3)
         # f_p.repeat(3, 1, n): image r (= 3b + v) is paired with f_p[r % B], as in the reference
         f_v_ = self.viewattn1(torch.cat([f_v, f_p.repeat(3, 1, f_v.size(2)).to(f_v.dtype)], 1))
