@@ -1,3 +1,5 @@
+# Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
+# stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
 O=gpurun_out/r4pm; mkdir -p $O
 export TMPDIR=/tmp
