@@ -11,7 +11,7 @@ from torch import nn
 from torch.autograd import Function
 from torch.amp import custom_bwd, custom_fwd
 
-from ._lib import call, lib, ptr, require_float, stream_of
+from ._lib import Workspace, call, lib, ptr, require_float, stream_of
 
 
 class chamfer_3DFunction(Function):
@@ -28,8 +28,15 @@ class chamfer_3DFunction(Function):
         idx1 = torch.empty(B, n, dtype=torch.int32, device=dev)
         idx2 = torch.empty(B, m, dtype=torch.int32, device=dev)
         with torch.cuda.device(dev):
-            call("chamfer_3D.forward", lib().pcops_chamfer_forward, ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist1),
-                 ptr(dist2), ptr(idx1), ptr(idx2), stream_of(xyz1))
+            # large clouds: the spatially culled search (scratch for the sorted clouds and tile boxes)
+            wsb = lib().pcops_chamfer_workspace_bytes(B, n, m)
+            if wsb:
+                ws = Workspace.get(dev, wsb)
+                call("chamfer_3D.forward", lib().pcops_chamfer_forward_ws, ptr(xyz1), ptr(xyz2), B, n, m,
+                     ptr(dist1), ptr(dist2), ptr(idx1), ptr(idx2), ptr(ws), wsb, stream_of(xyz1))
+            else:
+                call("chamfer_3D.forward", lib().pcops_chamfer_forward, ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist1),
+                     ptr(dist2), ptr(idx1), ptr(idx2), stream_of(xyz1))
         ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
         ctx.mark_non_differentiable(idx1, idx2)
         return dist1, dist2, idx1, idx2

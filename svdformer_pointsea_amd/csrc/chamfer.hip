@@ -610,6 +610,263 @@ __global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
   }
 }
 
+// ---------------------------------------------------------------- spatially culled
+// Large clouds (the loss's 16384^2): both clouds counting-sorted by a 16^3 Morton cell code of
+// their own box (chamfer_cull_prep_kernel), targets cut into tiles of kCullTS sorted points with
+// exact bounding boxes.  A block owns kCullQB consecutive sorted queries (a compact region): it
+// scans the tile nearest its box first, then the others outward in sorted order, skipping every
+// tile whose box lies farther than the block's largest current best distance.  Pairs are
+// evaluated with the reference expression (sqd3) and the winner kept in (distance, index)
+// order, lowest original index on ties -- the reference's bits and tie rule without its
+// index-order scan.  Skip test: the box distance lb (fp32) is shrunk by 64u before comparing,
+// which covers the fp32 rounding of both the box gaps and any pair's sqd3 (<= ~11u relative),
+// so a skipped tile holds no pair at or below the best; below 1e-30 nothing is skipped
+// (denormal scale).  A cloud with a non-finite coordinate disables the culling for its batch
+// (every tile scanned) and applies the reference's first-candidate rule: a NaN distance to
+// target 0 is kept with index 0 (chamfer3D.cu's best = d[0] start).
+constexpr int kCullQB = 256, kCullTS = 64, kCullMaxTiles = 1024, kCellBits = 4, kCells = 1 << (3 * kCellBits);
+
+__device__ __forceinline__ int cull_cell(float x, float y, float z, const float *g) {
+  auto ax = [](float v, float lo, float sc) {
+    const float t = fminf(fmaxf((v - lo) * sc, 0.f), float((1 << kCellBits) - 1));  // NaN -> 0
+    return (int)t;
+  };
+  const int cx = ax(x, g[0], g[3]), cy = ax(y, g[1], g[4]), cz = ax(z, g[2], g[5]);
+  int code = 0;
+#pragma unroll
+  for (int bit = 0; bit < kCellBits; ++bit)
+    code |= (((cx >> bit) & 1) << (3 * bit)) | (((cy >> bit) & 1) << (3 * bit + 1)) | (((cz >> bit) & 1) << (3 * bit + 2));
+  return code;
+}
+
+struct CullWs {
+  float4 *srt[2], *lo[2], *hi[2];
+  int *flag;
+};
+
+// grid (B, 2): cloud c (0 = xyz1, 1 = xyz2) of batch b -> sorted float4 (x, y, z, original index
+// bits), tile boxes, non-finite flag.  The order inside a cell comes from LDS atomics (any order
+// gives the same result, see above).
+__global__ __launch_bounds__(1024) void chamfer_cull_prep_kernel(const float *__restrict__ xyz1,
+                                                                 const float *__restrict__ xyz2, int N, int M,
+                                                                 CullWs ws) {
+  __shared__ int cnt[kCells];
+  __shared__ float red[6][16];
+  __shared__ float g[6];
+  __shared__ int wsum[16];
+  const int b = blockIdx.x, c = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = c ? M : N;
+  const float *pb = (c ? xyz2 : xyz1) + (size_t)b * n * 3;
+  float4 *srt = ws.srt[c] + (size_t)b * n;
+  const int nt = (n + kCullTS - 1) / kCullTS;
+  float4 *lo = ws.lo[c] + (size_t)b * nt, *hi = ws.hi[c] + (size_t)b * nt;
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int bad = 0;
+  for (int i = tid; i < n; i += 1024) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float x = pb[3 * i + a];
+      bad |= !(fabsf(x) < INFINITY);
+      v[a] = fminf(v[a], x);
+      v[3 + a] = fmaxf(v[3 + a], x);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    v[a] = a < 3 ? wave_min_f32(v[a]) : wave_max_f32(v[a]);
+    if (lane == 0) red[a][w] = v[a];
+  }
+  for (int k = tid; k < kCells; k += 1024) cnt[k] = 0;
+  bad = __syncthreads_or(bad);
+  if (tid < 3) {
+    float l = red[tid][0], h = red[3 + tid][0];
+    for (int j = 1; j < 16; ++j) {
+      l = fminf(l, red[tid][j]);
+      h = fmaxf(h, red[3 + tid][j]);
+    }
+    const float ext = h - l;
+    const bool ok = ext > 0.f && ext < INFINITY;
+    g[tid] = ok ? l : 0.f;
+    g[3 + tid] = ok ? float(1 << kCellBits) / ext : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024) atomicAdd(&cnt[cull_cell(pb[3 * i], pb[3 * i + 1], pb[3 * i + 2], g)], 1);
+  __syncthreads();
+  constexpr int PT = kCells / 1024;
+  int loc[PT], run = 0;
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    loc[j] = run;
+    run += cnt[tid * PT + j];
+  }
+  int incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = incl - run;
+  for (int j = 0; j < w; ++j) base += wsum[j];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) cnt[tid * PT + j] = base + loc[j];
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024) {
+    const float x = pb[3 * i], y = pb[3 * i + 1], z = pb[3 * i + 2];
+    const int pos = atomicAdd(&cnt[cull_cell(x, y, z, g)], 1);
+    srt[pos] = make_float4(x, y, z, __int_as_float(i));
+  }
+  __syncthreads();  // this block's sorted rows, written above, are read back below
+  for (int t = tid; t < nt; t += 1024) {
+    float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+    const int e = min(n, (t + 1) * kCullTS);
+    for (int k = t * kCullTS; k < e; ++k) {
+      const float4 p = srt[k];
+      l.x = fminf(l.x, p.x), l.y = fminf(l.y, p.y), l.z = fminf(l.z, p.z);
+      h.x = fmaxf(h.x, p.x), h.y = fmaxf(h.y, p.y), h.z = fmaxf(h.z, p.z);
+    }
+    lo[t] = l;
+    hi[t] = h;
+  }
+  if (tid == 0) ws.flag[b * 2 + c] = bad;
+}
+
+__device__ __forceinline__ float box_gap(float qlo, float qhi, float tlo, float thi) {
+  return fmaxf(0.f, fmaxf(tlo - qhi, qlo - thi));
+}
+
+// grid (blocks of dir 0 + blocks of dir 1, B), kCullQB threads: one sorted query per thread
+__global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__restrict__ xyz1,
+                                                               const float *__restrict__ xyz2, int N, int M,
+                                                               CullWs ws, float *__restrict__ dist1,
+                                                               float *__restrict__ dist2, int *__restrict__ idx1,
+                                                               int *__restrict__ idx2, int blocks_dir0) {
+  __shared__ float lb[kCullMaxTiles];
+  __shared__ float4 tile[kCullTS];
+  __shared__ float rq[6][kCullQB / 64];
+  __shared__ float rm[kCullQB / 64];
+  __shared__ int ri[kCullQB / 64];
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dir = (int)blockIdx.x >= blocks_dir0;
+  const int bx = dir ? blockIdx.x - blocks_dir0 : blockIdx.x;
+  const int NA = dir ? M : N, NT = dir ? N : M;
+  const float4 *A = ws.srt[dir] + (size_t)b * NA;
+  const float4 *T = ws.srt[1 - dir] + (size_t)b * NT;
+  const int nt = (NT + kCullTS - 1) / kCullTS;
+  const float4 *tlo = ws.lo[1 - dir] + (size_t)b * nt, *thi = ws.hi[1 - dir] + (size_t)b * nt;
+  const float *Torig = (dir ? xyz1 : xyz2) + (size_t)b * NT * 3;
+  float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
+  int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
+  const bool bad = ws.flag[b * 2] | ws.flag[b * 2 + 1];
+
+  const int qs = bx * kCullQB + tid;
+  const bool valid = qs < NA;
+  const float4 a = A[valid ? qs : NA - 1];
+  // the block's query box
+  float v[6] = {a.x, a.y, a.z, a.x, a.y, a.z};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    v[k] = k < 3 ? wave_min_f32(v[k]) : wave_max_f32(v[k]);
+    if (lane == 0) rq[k][w] = v[k];
+  }
+  __syncthreads();
+  float q[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    q[k] = rq[k][0];
+#pragma unroll
+    for (int j = 1; j < kCullQB / 64; ++j) q[k] = k < 3 ? fminf(q[k], rq[k][j]) : fmaxf(q[k], rq[k][j]);
+  }
+  // lower bounds of every target tile, and the nearest tile
+  float bl = INFINITY;
+  int bj = 0;
+  for (int t = tid; t < nt; t += kCullQB) {
+    const float4 l = tlo[t], h = thi[t];
+    const float gx = box_gap(q[0], q[3], l.x, h.x), gy = box_gap(q[1], q[4], l.y, h.y),
+                gz = box_gap(q[2], q[5], l.z, h.z);
+    const float d = (gx * gx + gy * gy) + gz * gz;
+    lb[t] = bad ? -INFINITY : d * (1.f - 64.f * kU);
+    if (d < bl) bl = d, bj = t;
+  }
+  {  // block argmin (first tile on equal bounds)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ol = __shfl_xor(bl, o);
+      const int oj = __shfl_xor(bj, o);
+      if (ol < bl || (ol == bl && oj < bj)) bl = ol, bj = oj;
+    }
+    if (lane == 0) rm[w] = bl, ri[w] = bj;
+  }
+  __syncthreads();
+  int j0 = ri[0];
+  float l0 = rm[0];
+  for (int k = 1; k < kCullQB / 64; ++k)
+    if (rm[k] < l0 || (rm[k] == l0 && ri[k] < j0)) l0 = rm[k], j0 = ri[k];
+
+  float best = INFINITY;
+  int bidx = INT_MAX;
+  auto process = [&](int j) {
+    __syncthreads();  // the previous tile's reads are done
+    if (tid < kCullTS) {
+      const int k = j * kCullTS + tid;
+      tile[tid] = k < NT ? T[k] : make_float4(NAN, NAN, NAN, __int_as_float(INT_MAX));
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < kCullTS; ++kk) {
+      const float4 t = tile[kk];
+      const float d = sqd3(t.x - a.x, t.y - a.y, t.z - a.z);
+      const int ti = __float_as_int(t.w);
+      if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
+    }
+  };
+  auto block_max_best = [&]() {
+    float m = wave_max_f32(valid ? best : -INFINITY);
+    __syncthreads();
+    if (lane == 0) rm[w] = m;
+    __syncthreads();
+    float r = rm[0];
+    for (int k = 1; k < kCullQB / 64; ++k) r = fmaxf(r, rm[k]);
+    return r;
+  };
+  process(j0);
+  float mb = block_max_best();
+  for (int s = 1; s < 2 * nt; ++s) {  // outward from j0: j0+1, j0-1, j0+2, ...
+    const int j = (s & 1) ? j0 + (s + 1) / 2 : j0 - s / 2;
+    if (j < 0 || j >= nt) continue;
+    const float lj = lb[j];
+    if (lj > mb && lj > 1e-30f) continue;  // uniform: every thread reads the same bound
+    process(j);
+    mb = block_max_best();
+  }
+  if (!valid) return;
+  if (bad) {
+    const float d0 = sqd3(Torig[0] - a.x, Torig[1] - a.y, Torig[2] - a.z);
+    if (d0 != d0) best = d0, bidx = 0;
+  }
+  if (bidx == INT_MAX) bidx = 0;
+  const int oq = __float_as_int(a.w);
+  dist[oq] = best;
+  idx[oq] = bidx;
+}
+
+size_t cull_ws_bytes(int B, int N, int M) {
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t nt1 = (N + kCullTS - 1) / kCullTS, nt2 = (M + kCullTS - 1) / kCullTS;
+  return al((size_t)B * N * 16) + al((size_t)B * M * 16) + 2 * al((size_t)B * nt1 * 16) + 2 * al((size_t)B * nt2 * 16) +
+         al((size_t)B * 8);
+}
+
+bool cull_applies(int N, int M) {
+  static const bool on = [] {  // PCOPS_CHAMFER_CULL=0: the all-pairs screens only (A/B)
+    const char *e = getenv("PCOPS_CHAMFER_CULL");
+    return !(e && e[0] == '0');
+  }();
+  return on && N >= 4096 && M >= 4096 && (N + kCullTS - 1) / kCullTS <= kCullMaxTiles &&
+         (M + kCullTS - 1) / kCullTS <= kCullMaxTiles;
+}
+
 }  // namespace
 
 extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B, int N, int M, float *dist1,
@@ -695,6 +952,39 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
   else
     hipLaunchKernelGGL(chamfer_nn_kernel<1>, grid, dim3(kThreads), 0, s, xyz1, xyz2, N, M, dist1, dist2, idx1, idx2,
                        b0);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" unsigned long long pcops_chamfer_workspace_bytes(int B, int N, int M) {
+  if (B <= 0 || N <= 0 || M <= 0 || !cull_applies(N, M)) return 0;
+  return cull_ws_bytes(B, N, M);
+}
+
+// pcops_chamfer_forward with scratch: large clouds take the spatially culled search (same
+// outputs bit for bit); anything else, or a short workspace, is pcops_chamfer_forward
+extern "C" int pcops_chamfer_forward_ws(const float *xyz1, const float *xyz2, int B, int N, int M, float *dist1,
+                                        float *dist2, int *idx1, int *idx2, void *workspace,
+                                        unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (B <= 0 || N <= 0 || M <= 0 || !cull_applies(N, M) || !workspace || workspace_bytes < cull_ws_bytes(B, N, M))
+    return pcops_chamfer_forward(xyz1, xyz2, B, N, M, dist1, dist2, idx1, idx2, stream);
+  if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2) return PCOPS_ERR_INVALID;
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  char *w = (char *)workspace;
+  const size_t nt1 = (N + kCullTS - 1) / kCullTS, nt2 = (M + kCullTS - 1) / kCullTS;
+  CullWs ws;
+  ws.srt[0] = (float4 *)w, w += al((size_t)B * N * 16);
+  ws.srt[1] = (float4 *)w, w += al((size_t)B * M * 16);
+  ws.lo[0] = (float4 *)w, w += al((size_t)B * nt1 * 16);
+  ws.hi[0] = (float4 *)w, w += al((size_t)B * nt1 * 16);
+  ws.lo[1] = (float4 *)w, w += al((size_t)B * nt2 * 16);
+  ws.hi[1] = (float4 *)w, w += al((size_t)B * nt2 * 16);
+  ws.flag = (int *)w;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(chamfer_cull_prep_kernel, dim3(B, 2), dim3(1024), 0, s, xyz1, xyz2, N, M, ws);
+  const int b0 = (N + kCullQB - 1) / kCullQB, b1 = (M + kCullQB - 1) / kCullQB;
+  hipLaunchKernelGGL(chamfer_cull_kernel, dim3(b0 + b1, B), dim3(kCullQB), 0, s, xyz1, xyz2, N, M, ws, dist1, dist2,
+                     idx1, idx2, b0);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

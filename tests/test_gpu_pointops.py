@@ -648,3 +648,66 @@ def test_knn3_adversarial_bitexact(dev, monkeypatch, B, S, N, K, pad, kind):
         oidx, od = O.knn(q, p, K, pad, return_dist=True)
         np.testing.assert_array_equal(got[0].cpu().numpy(), oidx)
         np.testing.assert_array_equal(got[1].cpu().numpy(), od)
+
+
+@pytest.mark.parametrize("B,N,M,kind", [(2, 16384, 16384, "gauss"), (3, 16384, 8192, "surface"),
+                                        (2, 8192, 8192, "dup"), (2, 4096, 20000, "clusters"),
+                                        (3, 6000, 5000, "nonfinite"), (2, 4096, 4096, "same"),
+                                        (2, 5000, 7000, "huge"), (2, 4096, 4100, "tiny"), (32, 16384, 16384, "pcn")])
+def test_chamfer_culled_bitexact(dev, B, N, M, kind):
+    """The spatially culled Chamfer search (pcops_chamfer_forward_ws: Morton-sorted clouds, tile
+    boxes, blocks skipping tiles beyond their current best under a rigorous margin) against the
+    all-pairs screens (pcops_chamfer_forward): dist and idx bitwise, both directions.  Exact
+    duplicates (ties across tiles), far clusters, NaN / inf points (culling off, the reference's
+    first-candidate rule), a single repeated point, coordinates whose squares overflow, and
+    coordinates whose distances are denormal."""
+    from svdformer_pointsea_amd._lib import Workspace, call, lib, ptr, stream_of
+
+    g = torch.Generator().manual_seed(B * N + M)
+    if kind in ("gauss", "pcn"):
+        a, b = torch.randn(B, N, 3, generator=g) * 0.45, torch.randn(B, M, 3, generator=g) * 0.45
+    elif kind == "surface":
+        def surf(n):
+            v = torch.randn(B, n, 3, generator=g)
+            return v / v.norm(dim=-1, keepdim=True) * torch.tensor([1.0, 0.6, 0.3])
+        a, b = surf(N), surf(M)
+    elif kind == "dup":
+        u = torch.randn(B, 1500, 3, generator=g)
+        a = u[:, torch.randint(0, 1500, (N,), generator=g)]
+        b = u[:, torch.randint(0, 1500, (M,), generator=g)]
+    elif kind == "clusters":
+        c = torch.randn(B, 6, 3, generator=g) * 50
+        a = c[:, torch.randint(0, 6, (N,), generator=g)] + 1e-2 * torch.randn(B, N, 3, generator=g)
+        b = c[:, torch.randint(0, 6, (M,), generator=g)] + 1e-2 * torch.randn(B, M, 3, generator=g)
+        a[:, ::997] = 1e4   # far outliers
+    elif kind == "nonfinite":
+        a, b = torch.randn(B, N, 3, generator=g), torch.randn(B, M, 3, generator=g)
+        a[0, 5, 1] = float("nan")
+        b[0, 0, 2] = float("inf")       # target 0: inf - inf / inf distances for every query
+        b[1, 7, 0] = float("-inf")
+        a[2, 0] = float("nan")
+    elif kind == "same":
+        a = torch.full((B, N, 3), 0.25)
+        b = torch.full((B, M, 3), 0.25)
+    elif kind == "huge":
+        a, b = torch.randn(B, N, 3, generator=g) * 1e19, torch.randn(B, M, 3, generator=g) * 1e19
+    else:
+        a, b = torch.randn(B, N, 3, generator=g) * 1e-20, torch.randn(B, M, 3, generator=g) * 1e-20
+    a, b = a.float().contiguous().to(dev), b.float().contiguous().to(dev)
+    outs = []
+    for ws_path in (False, True):
+        d1, d2 = torch.empty(B, N, device=dev), torch.empty(B, M, device=dev)
+        i1 = torch.empty(B, N, dtype=torch.int32, device=dev)
+        i2 = torch.empty(B, M, dtype=torch.int32, device=dev)
+        if ws_path:
+            wsb = lib().pcops_chamfer_workspace_bytes(B, N, M)
+            assert wsb > 0
+            ws = Workspace.get(a.device, wsb)
+            call("cull", lib().pcops_chamfer_forward_ws, ptr(a), ptr(b), B, N, M, ptr(d1), ptr(d2), ptr(i1), ptr(i2),
+                 ptr(ws), wsb, stream_of(a))
+        else:
+            call("screen", lib().pcops_chamfer_forward, ptr(a), ptr(b), B, N, M, ptr(d1), ptr(d2), ptr(i1), ptr(i2),
+                 stream_of(a))
+        outs.append((d1, d2, i1, i2))
+    for x, y in zip(*outs):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
