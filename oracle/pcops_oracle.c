@@ -278,7 +278,10 @@ EXPORT void oracle_three_interpolate_grad(int B, int C, int N, int M, const floa
 /* ------------------------------------------------------------------------ */
 /* NmDistanceKernel chamfer3D.cu:12-134, one direction: for every point of a,
  * the nearest point of b (squared distance) and the LOWEST index among equal
- * minima (strict '<' inside a 512-chunk, strict '>' across chunks). */
+ * minima: each 512-target chunk (:13,16) is seeded with its first target and
+ * updated on strict '<' (:36,46,121), the chunk results merged on strict '>'
+ * (:126) -- so a NaN distance at a chunk start pins (NaN, 0) for chunk 0 and
+ * hides a later chunk, as in the reference. */
 static void chamfer_dir(int B, int N, const float *a, int M, const float *bb, float *dist, int *idx) {
   /* every (b, j) output is independent: OpenMP over them changes no result */
 #pragma omp parallel for collapse(2) schedule(static)
@@ -289,11 +292,20 @@ static void chamfer_dir(int B, int N, const float *a, int M, const float *bb, fl
       const float x1 = pa[3 * j], y1 = pa[3 * j + 1], z1 = pa[3 * j + 2];
       float best = 0.f;
       int besti = 0;
-      for (int k = 0; k < M; ++k) {
-        const float d = sqd3(pb[3 * k] - x1, pb[3 * k + 1] - y1, pb[3 * k + 2] - z1);
-        if (k == 0 || d < best) {
-          best = d;
-          besti = k;
+      for (int k2 = 0; k2 < M; k2 += 512) {
+        const int end = k2 + 512 < M ? k2 + 512 : M;
+        float cb = 0.f;
+        int ci = k2;
+        for (int k = k2; k < end; ++k) {
+          const float d = sqd3(pb[3 * k] - x1, pb[3 * k + 1] - y1, pb[3 * k + 2] - z1);
+          if (k == k2 || d < cb) {
+            cb = d;
+            ci = k;
+          }
+        }
+        if (k2 == 0 || best > cb) {
+          best = cb;
+          besti = ci;
         }
       }
       if (M > 0) {

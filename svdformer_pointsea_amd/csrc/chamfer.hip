@@ -33,6 +33,43 @@ constexpr int kTile = 1024;
 constexpr int kSub = 32;
 constexpr int kThreads = 256;
 
+// The reference's own scan (chamfer3D.cu:16-129): 512-target chunks, each seeded with its
+// FIRST target and updated on strict '<', merged across chunks on strict '>'.  Its result
+// equals the lowest-index minimum over the non-NaN distances -- what the fast searches
+// compute -- unless a distance at a chunk start is NaN: then a NaN seed of chunk 0 pins
+// (NaN, 0), and a NaN seed of a later chunk hides that whole chunk.  For a finite query that
+// happens only for a target 512c with a NaN coordinate (finite - inf squares to inf, never
+// NaN), so the kernels send exactly the non-finite queries and the queries of a cloud with
+// such a target here.
+constexpr int kRefChunk = 512;
+
+__device__ __forceinline__ void ref_scan(const float *T, int NT, float ax, float ay, float az, float &res, int &ri) {
+  for (int k2 = 0; k2 < NT; k2 += kRefChunk) {
+    const int end = min(NT, k2 + kRefChunk);
+    float best = sqd3(T[3 * k2] - ax, T[3 * k2 + 1] - ay, T[3 * k2 + 2] - az);
+    int bi = k2;
+    for (int k = k2 + 1; k < end; ++k) {
+      const float d = sqd3(T[3 * k] - ax, T[3 * k + 1] - ay, T[3 * k + 2] - az);
+      if (d < best) best = d, bi = k;
+    }
+    if (k2 == 0 || res > best) res = best, ri = bi;
+  }
+}
+
+// block-uniform: does a chunk-start target (index 512c) have a NaN coordinate?
+__device__ bool nan_chunk_starts(const float *T, int NT) {
+  int f = 0;
+  for (int c = threadIdx.x; c * kRefChunk < NT; c += blockDim.x) {
+    const float *p = T + (size_t)3 * c * kRefChunk;
+    f |= (p[0] != p[0]) | (p[1] != p[1]) | (p[2] != p[2]);
+  }
+  return __syncthreads_or(f);
+}
+
+__device__ __forceinline__ bool finite3(float x, float y, float z) {
+  return fabsf(x) < INFINITY && fabsf(y) < INFINITY && fabsf(z) < INFINITY;
+}
+
 template <int Q>
 __global__ __launch_bounds__(kThreads) void chamfer_nn_kernel(const float *__restrict__ xyz1,
                                                               const float *__restrict__ xyz2, int N, int M,
@@ -48,6 +85,7 @@ __global__ __launch_bounds__(kThreads) void chamfer_nn_kernel(const float *__res
   float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
   int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
   if (NT <= 0) return;  // outputs keep the caller's zeros (chamfer3D.cu never writes them)
+  const bool nanst = nan_chunk_starts(T, NT);
 
   const int tid = threadIdx.x;
   float ax[Q], ay[Q], az[Q], best[Q];
@@ -103,6 +141,14 @@ __global__ __launch_bounds__(kThreads) void chamfer_nn_kernel(const float *__res
   for (int i = 0; i < Q; ++i) {
     const int qi = bx * kThreads * Q + i * kThreads + tid;
     if (qi >= NA) continue;
+    if (nanst || !finite3(ax[i], ay[i], az[i])) {
+      float r = 0.f;
+      int rk = 0;
+      ref_scan(T, NT, ax[i], ay[i], az[i], r, rk);
+      dist[qi] = r;
+      idx[qi] = rk;
+      continue;
+    }
     int bk = bs[i];
     const int end = min(bs[i] + kSub, NT);
     for (int k = bs[i]; k < end; ++k) {
@@ -161,6 +207,7 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
   float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
   int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
   if (NT <= 0) return;
+  const bool nanst = nan_chunk_starts(T, NT);
 
   const int tid = threadIdx.x;
   float ax[Q], ay[Q], az[Q], an[Q], anorm[Q], mine[Q], slack[Q];
@@ -266,6 +313,12 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
     if (qi >= NA) continue;
     float best = INFINITY;
     int bk = 0;
+    if (nanst || !finite3(ax[i], ay[i], az[i])) {
+      ref_scan(T, NT, ax[i], ay[i], az[i], best, bk);
+      dist[qi] = best;
+      idx[qi] = bk;
+      continue;
+    }
     if (!over[i]) {
 #pragma unroll
       for (int c = 0; c < kSlots; ++c) {
@@ -325,6 +378,7 @@ __global__ __launch_bounds__(kThreads) void chamfer_mfma_kernel(const float *__r
   float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
   int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
   if (NT <= 0) return;
+  const bool nanst = nan_chunk_starts(T, NT);
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, w = tid >> 6;
   const int qi = bx * (kThreads / 2) + w * 32 + (lane & 31);
@@ -420,6 +474,12 @@ __global__ __launch_bounds__(kThreads) void chamfer_mfma_kernel(const float *__r
   // exact re-derivation with the reference expression (chamfer_screen_kernel's)
   float best = INFINITY;
   int bk = 0;
+  if (nanst || !finite3(ax, ay, az)) {
+    ref_scan(T, NT, ax, ay, az, best, bk);
+    dist[qi] = best;
+    idx[qi] = bk;
+    return;
+  }
   if (!over) {
 #pragma unroll
     for (int c = 0; c < kSlots; ++c) {
@@ -840,11 +900,9 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
     process(j);
     mb = block_max_best();
   }
+  const bool nanst = bad && nan_chunk_starts(Torig, NT);  // block-uniform
   if (!valid) return;
-  if (bad) {
-    const float d0 = sqd3(Torig[0] - a.x, Torig[1] - a.y, Torig[2] - a.z);
-    if (d0 != d0) best = d0, bidx = 0;
-  }
+  if (nanst || !finite3(a.x, a.y, a.z)) ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
   if (bidx == INT_MAX) bidx = 0;
   const int oq = __float_as_int(a.w);
   dist[oq] = best;
@@ -894,7 +952,7 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
   const int b0 = (N + kThreads * Q - 1) / (kThreads * Q);
   const int b1 = (M + kThreads * Q - 1) / (kThreads * Q);
   const dim3 grid(b0 + b1, B);
-  static const bool screen = [] {  // PCOPS_CHAMFER_SCREEN=0: the direct kernel (A/B runs)
+  const bool screen = [] {  // PCOPS_CHAMFER_SCREEN=0: the direct kernel (A/B runs, tests)
     const char *e = getenv("PCOPS_CHAMFER_SCREEN");
     return !(e && e[0] == '0');
   }();
@@ -903,7 +961,7 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
   // same box), 2 = everywhere: at 16384^2 alone it ties the Q = 4 VALU screen (1.67 vs 1.69 ms), in
   // the step it measured 0.4-0.8 ms slower (it shares the matrix cores with the concurrent GEMMs /
   // attention of the other stream); profiles/r3_chamfer_mfma_ab.txt
-  static const int mfma = [] {
+  const int mfma = [] {
     const char *e = getenv("PCOPS_CHAMFER_MFMA");
     return e ? atoi(e) : 1;
   }();

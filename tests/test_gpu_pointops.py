@@ -379,6 +379,38 @@ def test_chamfer_screen_bitexact(dev, monkeypatch, kind, q):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("kernel", [{}, {"PCOPS_CHAMFER_Q": "2"}, {"PCOPS_CHAMFER_Q": "4"},
+                                    {"PCOPS_CHAMFER_SCREEN": "0"}, {"PCOPS_CHAMFER_Q": "4", "PCOPS_CHAMFER_MFMA": "2"}])
+def test_chamfer_nonfinite_scan_order(dev, monkeypatch, kernel):
+    """The reference's chunked scan order on non-finite data (chamfer3D.cu:16-129), every
+    forward kernel (MFMA screen, VALU screen Q=2/4, direct) against the oracle, bitwise: a NaN
+    coordinate on a chunk-start target (index 512c) pins (NaN, 0) for c = 0 and hides chunk c
+    otherwise; NaN off a chunk start, inf targets and non-finite queries."""
+    from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
+
+    for k, v in kernel.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(23)
+    B, N, M = 4, 1100, 1600
+    a = (rng.random((B, N, 3)) - 0.5).astype(np.float32)
+    b = (rng.random((B, M, 3)) - 0.5).astype(np.float32)
+    b[0, 0, 1] = np.nan
+    a[0, 1024, 0] = np.nan
+    b[1, 512, 0] = np.nan
+    b[1, 1024, 2] = np.inf
+    a[1, 0, 2] = np.nan
+    b[2, 513] = np.nan
+    b[2, 0, 0] = np.inf
+    a[2, 3] = [np.inf, 0.0, 0.0]
+    a[3, 5, 1] = np.nan
+    b[3, 1536, 1] = np.nan
+    got = [t.cpu().numpy() for t in chamfer_3DDist()(T(a, dev), T(b, dev))]
+    ref = O.chamfer_forward(a, b)
+    for x, y in zip(got, ref):
+        np.testing.assert_array_equal(x, y)
+    assert np.isnan(got[0][0]).all() and np.isnan(got[1][1]).all()
+
+
 def test_chamfer_full_size_one_cloud_bitexact(dev):
     """16384 x 16384 (the loss Chamfer, screened kernel) on one cloud, both directions, vs the oracle."""
     from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
@@ -685,6 +717,7 @@ def test_chamfer_culled_bitexact(dev, B, N, M, kind):
         a[0, 5, 1] = float("nan")
         b[0, 0, 2] = float("inf")       # target 0: inf - inf / inf distances for every query
         b[1, 7, 0] = float("-inf")
+        b[1, 1536, 1] = float("nan")    # a chunk-start target: chunk 3 hidden (reference scan order)
         a[2, 0] = float("nan")
     elif kind == "same":
         a = torch.full((B, N, 3), 0.25)
@@ -711,3 +744,6 @@ def test_chamfer_culled_bitexact(dev, B, N, M, kind):
         outs.append((d1, d2, i1, i2))
     for x, y in zip(*outs):
         np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+    if kind == "nonfinite":
+        for x, y in zip(outs[1], O.chamfer_forward(a.cpu().numpy(), b.cpu().numpy())):
+            np.testing.assert_array_equal(x.cpu().numpy(), y)

@@ -68,6 +68,54 @@ def test_chamfer_oracle_matches_reference_python():
         np.testing.assert_array_equal(i2, g[name + "_i2"])
 
 
+def _nm_distance_literal(a, b):
+    """NmDistanceKernel (chamfer3D.cu:12-134) as a literal loop: 512-target chunks, the chunk
+    seeded by its first target (`k==0 || d<best`), merged by `k2==0 || result>best`."""
+    n, m = len(a), len(b)
+    res, ri = [0.0] * n, [0] * n
+    for j in range(n):
+        x1, y1, z1 = (float(v) for v in a[j])
+        for k2 in range(0, m, 512):
+            best, best_i = 0.0, 0
+            for k in range(min(m, k2 + 512) - k2):
+                x2, y2, z2 = float(b[k2 + k][0]) - x1, float(b[k2 + k][1]) - y1, float(b[k2 + k][2]) - z1
+                d = x2 * x2 + y2 * y2 + z2 * z2
+                if k == 0 or d < best:
+                    best, best_i = d, k + k2
+            if k2 == 0 or res[j] > best:
+                res[j], ri[j] = best, best_i
+    return np.array(res, np.float32), np.array(ri, np.int32)
+
+
+def test_chamfer_oracle_nonfinite_scan_order():
+    """NaN at a chunk start: chunk 0's NaN seed pins (NaN, 0), a later chunk's hides that chunk;
+    NaN elsewhere, inf points and non-finite queries.  Small-integer coordinates, so every
+    distance is exact and the literal float64 loop is the reference's fp32 arithmetic."""
+    rng = np.random.default_rng(17)
+    B, N, M = 4, 70, 1100
+    a = rng.integers(0, 8, (B, N, 3)).astype(np.float32)
+    b = rng.integers(0, 8, (B, M, 3)).astype(np.float32)
+    b[0, 0, 1] = np.nan                   # dir 0, chunk 0 seed
+    b[1, 512, 0] = np.nan                 # dir 0, chunk 1 seed: chunk 1 hidden
+    b[1, 1024, 2] = np.inf
+    a[1, 0, 2] = np.nan                   # dir 1, chunk 0 seed
+    b[2, 513] = np.nan                    # not a seed: skipped alone
+    b[2, 0, 0] = np.inf
+    a[2, 3] = [np.inf, 0.0, 0.0]          # inf query
+    a[3, 5, 1] = np.nan                   # NaN query
+    b[3, 1024, 1] = np.nan                # dir 0, chunk 2 seed (the short last chunk)
+    d1, d2, i1, i2 = O.chamfer_forward(a, b)
+    for bi in range(B):
+        rd1, ri1 = _nm_distance_literal(a[bi], b[bi])
+        rd2, ri2 = _nm_distance_literal(b[bi], a[bi])
+        np.testing.assert_array_equal(d1[bi], rd1)
+        np.testing.assert_array_equal(i1[bi], ri1)
+        np.testing.assert_array_equal(d2[bi], rd2)
+        np.testing.assert_array_equal(i2[bi], ri2)
+    assert np.isnan(d1[0]).all() and (i1[0] == 0).all()
+    assert np.isnan(d2[1]).all()
+
+
 def test_chamfer_backward_oracle_matches_finite_differences():
     rng = np.random.default_rng(9)
     a = (rng.random((1, 40, 3))).astype(np.float32)
