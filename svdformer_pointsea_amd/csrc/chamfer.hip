@@ -264,6 +264,9 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
     for (int i = 0; i < Q; ++i) {
       eps[i] = 16.f * kU * (eps_t2 + anorm[i] * tm);
       slack[i] = screen_slack(mine[i], an[i], eps[i]);  // eps only grows: re-derive
+      // |e| <= Tm^2 + 2|a|Tm: near fp32 overflow e may be +-inf / NaN and the margin
+      // meaningless -> direct scan
+      over[i] = over[i] || !(eps_t2 + 2.f * anorm[i] * tm < 1e38f);
     }
     const int nsub = (cnt + kSub - 1) / kSub;
     for (int sb = 0; sb < nsub; ++sb) {
@@ -425,6 +428,7 @@ __global__ __launch_bounds__(kThreads) void chamfer_mfma_kernel(const float *__r
     const float tm = sqrtf(eps_t2);
     const float eps = 16.f * kU * (eps_t2 + anorm * tm) + 1e-35f;
     slack = screen_slack(mine, an, eps);
+    over = over || !(eps_t2 + 2.f * anorm * tm < 1e38f);  // near fp32 overflow: direct scan
     const int nsub = (cnt + kSubM - 1) / kSubM;
     for (int sb = 0; sb < nsub; ++sb) {
       // kSubM / 32 independent 32 x 32 tiles, then one keep test for the kSubM targets

@@ -744,6 +744,6 @@ def test_chamfer_culled_bitexact(dev, B, N, M, kind):
         outs.append((d1, d2, i1, i2))
     for x, y in zip(*outs):
         np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
-    if kind == "nonfinite":
+    if kind in ("nonfinite", "huge", "tiny"):  # and against the oracle
         for x, y in zip(outs[1], O.chamfer_forward(a.cpu().numpy(), b.cpu().numpy())):
             np.testing.assert_array_equal(x.cpu().numpy(), y)
