@@ -677,17 +677,16 @@ __global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
 // ---------------------------------------------------------------- spatially culled
 // Large clouds (the loss's 16384^2): both clouds counting-sorted by a 16^3 Morton cell code of
 // their own box (chamfer_cull_prep_kernel), targets cut into tiles of kCullTS sorted points with
-// exact bounding boxes.  A block owns kCullQB consecutive sorted queries (a compact region): it
+// exact bounding boxes.  A wave owns 64 consecutive sorted queries (a compact region): it
 // scans the tile nearest its box first, then the others outward in sorted order, skipping every
-// tile whose box lies farther than the block's largest current best distance.  Pairs are
+// tile whose box lies farther than the wave's largest current best distance.  Pairs are
 // evaluated with the reference expression (sqd3) and the winner kept in (distance, index)
 // order, lowest original index on ties -- the reference's bits and tie rule without its
 // index-order scan.  Skip test: the box distance lb (fp32) is shrunk by 64u before comparing,
 // which covers the fp32 rounding of both the box gaps and any pair's sqd3 (<= ~11u relative),
 // so a skipped tile holds no pair at or below the best; below 1e-30 nothing is skipped
 // (denormal scale).  A cloud with a non-finite coordinate disables the culling for its batch
-// (every tile scanned) and applies the reference's first-candidate rule: a NaN distance to
-// target 0 is kept with index 0 (chamfer3D.cu's best = d[0] start).
+// (every tile scanned) and sends the queries ref_scan covers there.
 constexpr int kCullQB = 256, kCullTS = 64, kCullMaxTiles = 1024, kCellBits = 4, kCells = 1 << (3 * kCellBits);
 
 __device__ __forceinline__ int cull_cell(float x, float y, float z, const float *g) {
@@ -800,17 +799,17 @@ __device__ __forceinline__ float box_gap(float qlo, float qhi, float tlo, float 
   return fmaxf(0.f, fmaxf(tlo - qhi, qlo - thi));
 }
 
-// grid (blocks of dir 0 + blocks of dir 1, B), kCullQB threads: one sorted query per thread
+// grid (blocks of dir 0 + blocks of dir 1, B), kCullQB threads: one sorted query per lane.  Each
+// wave is an independent searcher over its 64 queries (its own box, bounds, tile buffer and
+// skip decisions): no block barriers, and a 64-query box is ~4x tighter than a block's.
 __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__restrict__ xyz1,
                                                                const float *__restrict__ xyz2, int N, int M,
                                                                CullWs ws, float *__restrict__ dist1,
                                                                float *__restrict__ dist2, int *__restrict__ idx1,
                                                                int *__restrict__ idx2, int blocks_dir0) {
-  __shared__ float lb[kCullMaxTiles];
-  __shared__ float4 tile[kCullTS];
-  __shared__ float rq[6][kCullQB / 64];
-  __shared__ float rm[kCullQB / 64];
-  __shared__ int ri[kCullQB / 64];
+  constexpr int W = kCullQB / 64;
+  __shared__ float lbs[W][kCullMaxTiles];
+  __shared__ float4 tiles[W][kCullTS];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int dir = (int)blockIdx.x >= blocks_dir0;
   const int bx = dir ? blockIdx.x - blocks_dir0 : blockIdx.x;
@@ -823,60 +822,44 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
   float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
   int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
   const bool bad = ws.flag[b * 2] | ws.flag[b * 2 + 1];
+  const bool nanst = bad && nan_chunk_starts(Torig, NT);  // block-uniform, before any wave exits
+  const int q0 = (bx * W + w) * 64;
+  if (q0 >= NA) return;  // whole wave past the end
 
-  const int qs = bx * kCullQB + tid;
+  const int qs = q0 + lane;
   const bool valid = qs < NA;
   const float4 a = A[valid ? qs : NA - 1];
-  // the block's query box
-  float v[6] = {a.x, a.y, a.z, a.x, a.y, a.z};
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    v[k] = k < 3 ? wave_min_f32(v[k]) : wave_max_f32(v[k]);
-    if (lane == 0) rq[k][w] = v[k];
-  }
-  __syncthreads();
-  float q[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    q[k] = rq[k][0];
-#pragma unroll
-    for (int j = 1; j < kCullQB / 64; ++j) q[k] = k < 3 ? fminf(q[k], rq[k][j]) : fmaxf(q[k], rq[k][j]);
-  }
+  // the wave's query box
+  const float qx0 = wave_min_f32(a.x), qy0 = wave_min_f32(a.y), qz0 = wave_min_f32(a.z);
+  const float qx1 = wave_max_f32(a.x), qy1 = wave_max_f32(a.y), qz1 = wave_max_f32(a.z);
   // lower bounds of every target tile, and the nearest tile
+  float *lb = lbs[w];
+  float4 *tile = tiles[w];
   float bl = INFINITY;
   int bj = 0;
-  for (int t = tid; t < nt; t += kCullQB) {
+  for (int t = lane; t < nt; t += 64) {
     const float4 l = tlo[t], h = thi[t];
-    const float gx = box_gap(q[0], q[3], l.x, h.x), gy = box_gap(q[1], q[4], l.y, h.y),
-                gz = box_gap(q[2], q[5], l.z, h.z);
+    const float gx = box_gap(qx0, qx1, l.x, h.x), gy = box_gap(qy0, qy1, l.y, h.y), gz = box_gap(qz0, qz1, l.z, h.z);
     const float d = (gx * gx + gy * gy) + gz * gz;
     lb[t] = bad ? -INFINITY : d * (1.f - 64.f * kU);
     if (d < bl) bl = d, bj = t;
   }
-  {  // block argmin (first tile on equal bounds)
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const float ol = __shfl_xor(bl, o);
-      const int oj = __shfl_xor(bj, o);
-      if (ol < bl || (ol == bl && oj < bj)) bl = ol, bj = oj;
-    }
-    if (lane == 0) rm[w] = bl, ri[w] = bj;
+  for (int o = 32; o >= 1; o >>= 1) {  // wave argmin (first tile on equal bounds)
+    const float ol = __shfl_xor(bl, o);
+    const int oj = __shfl_xor(bj, o);
+    if (ol < bl || (ol == bl && oj < bj)) bl = ol, bj = oj;
   }
-  __syncthreads();
-  int j0 = ri[0];
-  float l0 = rm[0];
-  for (int k = 1; k < kCullQB / 64; ++k)
-    if (rm[k] < l0 || (rm[k] == l0 && ri[k] < j0)) l0 = rm[k], j0 = ri[k];
+  const int j0 = __builtin_amdgcn_readfirstlane(bj);
 
   float best = INFINITY;
   int bidx = INT_MAX;
   auto process = [&](int j) {
-    __syncthreads();  // the previous tile's reads are done
-    if (tid < kCullTS) {
-      const int k = j * kCullTS + tid;
-      tile[tid] = k < NT ? T[k] : make_float4(NAN, NAN, NAN, __int_as_float(INT_MAX));
-    }
-    __syncthreads();
+    // one wave: its LDS accesses complete in issue order, the wave barrier keeps the compiler's
+    __builtin_amdgcn_wave_barrier();
+    const int k = j * kCullTS + lane;
+    tile[lane] = k < NT ? T[k] : make_float4(NAN, NAN, NAN, __int_as_float(INT_MAX));
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll 8
     for (int kk = 0; kk < kCullTS; ++kk) {
       const float4 t = tile[kk];
@@ -885,26 +868,19 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
       if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
     }
   };
-  auto block_max_best = [&]() {
-    float m = wave_max_f32(valid ? best : -INFINITY);
-    __syncthreads();
-    if (lane == 0) rm[w] = m;
-    __syncthreads();
-    float r = rm[0];
-    for (int k = 1; k < kCullQB / 64; ++k) r = fmaxf(r, rm[k]);
-    return r;
+  auto wave_best = [&]() {  // the wave's largest current best, as a scalar
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_f32(valid ? best : -INFINITY))));
   };
   process(j0);
-  float mb = block_max_best();
+  float mb = wave_best();
   for (int s = 1; s < 2 * nt; ++s) {  // outward from j0: j0+1, j0-1, j0+2, ...
     const int j = (s & 1) ? j0 + (s + 1) / 2 : j0 - s / 2;
     if (j < 0 || j >= nt) continue;
     const float lj = lb[j];
-    if (lj > mb && lj > 1e-30f) continue;  // uniform: every thread reads the same bound
+    if (lj > mb && lj > 1e-30f) continue;  // wave-uniform
     process(j);
-    mb = block_max_best();
+    mb = wave_best();
   }
-  const bool nanst = bad && nan_chunk_starts(Torig, NT);  // block-uniform
   if (!valid) return;
   if (nanst || !finite3(a.x, a.y, a.z)) ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
   if (bidx == INT_MAX) bidx = 0;
