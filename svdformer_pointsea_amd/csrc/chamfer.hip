@@ -23,6 +23,7 @@
 // combined with the target's own term.  Scattered float atomics (one lane per
 // 12-B row) ran at the ~0.08 TB/s one-row-per-lane atomic rate; the old
 // two-kernel atomic form stays behind PCOPS_CHAMFER_BWD=atomic for A/B runs.
+#include <cfloat>
 #include <cstdlib>
 
 #include "common.h"
@@ -687,7 +688,7 @@ __global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
 // so a skipped tile holds no pair at or below the best; below 1e-30 nothing is skipped
 // (denormal scale).  A cloud with a non-finite coordinate disables the culling for its batch
 // (every tile scanned) and sends the queries ref_scan covers there.
-constexpr int kCullQB = 256, kCullTS = 64, kCullMaxTiles = 1024, kCellBits = 4, kCells = 1 << (3 * kCellBits);
+constexpr int kCullQB = 256, kCullTS = 32, kCullMaxTiles = 512, kCellBits = 4, kCells = 1 << (3 * kCellBits);
 
 __device__ __forceinline__ int cull_cell(float x, float y, float z, const float *g) {
   auto ax = [](float v, float lo, float sc) {
@@ -807,8 +808,7 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
                                                                CullWs ws, float *__restrict__ dist1,
                                                                float *__restrict__ dist2, int *__restrict__ idx1,
                                                                int *__restrict__ idx2, int blocks_dir0) {
-  constexpr int W = kCullQB / 64;
-  __shared__ float lbs[W][kCullMaxTiles];
+  constexpr int W = kCullQB / 64, kLbRegs = kCullMaxTiles / 64;
   __shared__ float4 tiles[W][kCullTS];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int dir = (int)blockIdx.x >= blocks_dir0;
@@ -832,54 +832,69 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
   // the wave's query box
   const float qx0 = wave_min_f32(a.x), qy0 = wave_min_f32(a.y), qz0 = wave_min_f32(a.z);
   const float qx1 = wave_max_f32(a.x), qy1 = wave_max_f32(a.y), qz1 = wave_max_f32(a.z);
-  // lower bounds of every target tile, and the nearest tile
-  float *lb = lbs[w];
-  float4 *tile = tiles[w];
-  float bl = INFINITY;
-  int bj = 0;
-  for (int t = lane; t < nt; t += 64) {
-    const float4 l = tlo[t], h = thi[t];
-    const float gx = box_gap(qx0, qx1, l.x, h.x), gy = box_gap(qy0, qy1, l.y, h.y), gz = box_gap(qz0, qz1, l.z, h.z);
-    const float d = (gx * gx + gy * gy) + gz * gz;
-    lb[t] = bad ? -INFINITY : d * (1.f - 64.f * kU);
-    if (d < bl) bl = d, bj = t;
-  }
+  // lower bounds of the wave's box to every target tile, tile t = lane + 64 i in L[i]; clamped
+  // to FLT_MAX so that +inf marks a tile already taken
+  float L[kLbRegs];
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {  // wave argmin (first tile on equal bounds)
-    const float ol = __shfl_xor(bl, o);
-    const int oj = __shfl_xor(bj, o);
-    if (ol < bl || (ol == bl && oj < bj)) bl = ol, bj = oj;
+  for (int i = 0; i < kLbRegs; ++i) {
+    const int t = lane + 64 * i;
+    L[i] = INFINITY;
+    if (t < nt) {
+      const float4 l = tlo[t], h = thi[t];
+      const float gx = box_gap(qx0, qx1, l.x, h.x), gy = box_gap(qy0, qy1, l.y, h.y), gz = box_gap(qz0, qz1, l.z, h.z);
+      L[i] = bad ? -INFINITY : fminf((gx * gx + gy * gy) + gz * gz, FLT_MAX) * (1.f - 64.f * kU);
+    }
   }
-  const int j0 = __builtin_amdgcn_readfirstlane(bj);
 
+  float4 *tile = tiles[w];
   float best = INFINITY;
   int bidx = INT_MAX;
-  auto process = [&](int j) {
-    // one wave: its LDS accesses complete in issue order, the wave barrier keeps the compiler's
+  float mb = INFINITY;  // the wave's largest current best (scalar)
+  for (;;) {
+    // the untaken tile of smallest bound (first tile on equal bounds): nearest-first order
+    float m = INFINITY;
+    int mi = 0;
+#pragma unroll
+    for (int i = 0; i < kLbRegs; ++i)
+      if (L[i] < m) m = L[i], mi = i;
+    int t = lane + 64 * mi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float om = __shfl_xor(m, o);
+      const int ot = __shfl_xor(t, o);
+      if (om < m || (om == m && ot < t)) m = om, t = ot;
+    }
+    m = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (m == INFINITY) break;              // every tile taken
+    if (m > mb && m > 1e-30f) break;       // every untaken tile lies beyond every query's best
+    if (lane == (t & 63)) {
+#pragma unroll
+      for (int i = 0; i < kLbRegs; ++i)
+        if (i == (t >> 6)) L[i] = INFINITY;
+    }
+    // per-query test against the tile's box: the tile is read only if some query may improve
+    const float4 l = tlo[t], h = thi[t];
+    const float px = fmaxf(0.f, fmaxf(l.x - a.x, a.x - h.x)), py = fmaxf(0.f, fmaxf(l.y - a.y, a.y - h.y)),
+                pz = fmaxf(0.f, fmaxf(l.z - a.z, a.z - h.z));
+    const float pl = ((px * px + py * py) + pz * pz) * (1.f - 64.f * kU);
+    const bool need = valid && (bad || !(pl > best) || pl <= 1e-30f);
+    if (!__any(need)) continue;
+    // one wave: its LDS accesses complete in issue order, the wave barriers keep the compiler's
     __builtin_amdgcn_wave_barrier();
-    const int k = j * kCullTS + lane;
-    tile[lane] = k < NT ? T[k] : make_float4(NAN, NAN, NAN, __int_as_float(INT_MAX));
+    if (lane < kCullTS) {
+      const int k = t * kCullTS + lane;
+      tile[lane] = k < NT ? T[k] : make_float4(NAN, NAN, NAN, __int_as_float(INT_MAX));
+    }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll 8
     for (int kk = 0; kk < kCullTS; ++kk) {
-      const float4 t = tile[kk];
-      const float d = sqd3(t.x - a.x, t.y - a.y, t.z - a.z);
-      const int ti = __float_as_int(t.w);
+      const float4 p = tile[kk];
+      const float d = sqd3(p.x - a.x, p.y - a.y, p.z - a.z);
+      const int ti = __float_as_int(p.w);
       if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
     }
-  };
-  auto wave_best = [&]() {  // the wave's largest current best, as a scalar
-    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_f32(valid ? best : -INFINITY))));
-  };
-  process(j0);
-  float mb = wave_best();
-  for (int s = 1; s < 2 * nt; ++s) {  // outward from j0: j0+1, j0-1, j0+2, ...
-    const int j = (s & 1) ? j0 + (s + 1) / 2 : j0 - s / 2;
-    if (j < 0 || j >= nt) continue;
-    const float lj = lb[j];
-    if (lj > mb && lj > 1e-30f) continue;  // wave-uniform
-    process(j);
-    mb = wave_best();
+    mb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_f32(valid ? best : -INFINITY))));
   }
   if (!valid) return;
   if (nanst || !finite3(a.x, a.y, a.z)) ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
