@@ -1,7 +1,7 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r4ch3; mkdir -p $O
+O=gpurun_out/r4ch4; mkdir -p $O
 export TMPDIR=/tmp
 export PYTEST_K="culled or nonfinite_scan or chamfer_screen"
 bash tools/gpu_run.sh $O tests_k || exit 1
