@@ -810,6 +810,7 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
                                                                int *__restrict__ idx2, int blocks_dir0) {
   constexpr int W = kCullQB / 64, kLbRegs = kCullMaxTiles / 64;
   __shared__ float4 tiles[W][kCullTS];
+  __shared__ float4 blo[kCullMaxTiles], bhi[kCullMaxTiles];  // the target tiles' boxes
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int dir = (int)blockIdx.x >= blocks_dir0;
   const int bx = dir ? blockIdx.x - blocks_dir0 : blockIdx.x;
@@ -822,6 +823,8 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
   float *dist = (dir ? dist2 : dist1) + (size_t)b * NA;
   int *idx = (dir ? idx2 : idx1) + (size_t)b * NA;
   const bool bad = ws.flag[b * 2] | ws.flag[b * 2 + 1];
+  for (int t = tid; t < nt; t += kCullQB) blo[t] = tlo[t], bhi[t] = thi[t];
+  __syncthreads();
   const bool nanst = bad && nan_chunk_starts(Torig, NT);  // block-uniform, before any wave exits
   const int q0 = (bx * W + w) * 64;
   if (q0 >= NA) return;  // whole wave past the end
@@ -840,24 +843,19 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
     const int t = lane + 64 * i;
     L[i] = INFINITY;
     if (t < nt) {
-      const float4 l = tlo[t], h = thi[t];
+      const float4 l = blo[t], h = bhi[t];
       const float gx = box_gap(qx0, qx1, l.x, h.x), gy = box_gap(qy0, qy1, l.y, h.y), gz = box_gap(qz0, qz1, l.z, h.z);
       L[i] = bad ? -INFINITY : fminf((gx * gx + gy * gy) + gz * gz, FLT_MAX) * (1.f - 64.f * kU);
     }
   }
-
-  float4 *tile = tiles[w];
-  float best = INFINITY;
-  int bidx = INT_MAX;
-  float mb = INFINITY;  // the wave's largest current best (scalar)
-  for (;;) {
-    // the untaken tile of smallest bound (first tile on equal bounds): nearest-first order
-    float m = INFINITY;
+  // take the untaken tile of smallest bound (first tile on equal bounds): nearest-first order
+  auto take = [&](float &m, int &t) {
+    m = INFINITY;
     int mi = 0;
 #pragma unroll
     for (int i = 0; i < kLbRegs; ++i)
       if (L[i] < m) m = L[i], mi = i;
-    int t = lane + 64 * mi;
+    t = lane + 64 * mi;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       const float om = __shfl_xor(m, o);
@@ -866,15 +864,34 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
     }
     m = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
     t = __builtin_amdgcn_readfirstlane(t);
-    if (m == INFINITY) break;              // every tile taken
-    if (m > mb && m > 1e-30f) break;       // every untaken tile lies beyond every query's best
     if (lane == (t & 63)) {
 #pragma unroll
       for (int i = 0; i < kLbRegs; ++i)
         if (i == (t >> 6)) L[i] = INFINITY;
     }
-    // per-query test against the tile's box: the tile is read only if some query may improve
-    const float4 l = tlo[t], h = thi[t];
+  };
+  auto fetch = [&](float m, int t) {  // the tile's points, one per lane (issued a tile ahead)
+    const int k = t * kCullTS + lane;
+    return (m < INFINITY && lane < kCullTS && k < NT) ? T[k] : make_float4(NAN, NAN, NAN, __int_as_float(INT_MAX));
+  };
+
+  float4 *tile = tiles[w];
+  float best = INFINITY;
+  int bidx = INT_MAX;
+  float mb = INFINITY;  // the wave's largest current best (scalar)
+  float m;
+  int t;
+  take(m, t);
+  float4 pf = fetch(m, t);
+  for (;;) {
+    if (m == INFINITY) break;         // every tile taken
+    if (m > mb && m > 1e-30f) break;  // every untaken tile lies beyond every query's best
+    const int tc = t;
+    const float4 cur = pf;
+    take(m, t);  // the next tile, its points in flight while this one is scanned
+    pf = fetch(m, t);
+    // per-query test against the tile's box: the tile is scanned only if some query may improve
+    const float4 l = blo[tc], h = bhi[tc];
     const float px = fmaxf(0.f, fmaxf(l.x - a.x, a.x - h.x)), py = fmaxf(0.f, fmaxf(l.y - a.y, a.y - h.y)),
                 pz = fmaxf(0.f, fmaxf(l.z - a.z, a.z - h.z));
     const float pl = ((px * px + py * py) + pz * pz) * (1.f - 64.f * kU);
@@ -882,10 +899,7 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
     if (!__any(need)) continue;
     // one wave: its LDS accesses complete in issue order, the wave barriers keep the compiler's
     __builtin_amdgcn_wave_barrier();
-    if (lane < kCullTS) {
-      const int k = t * kCullTS + lane;
-      tile[lane] = k < NT ? T[k] : make_float4(NAN, NAN, NAN, __int_as_float(INT_MAX));
-    }
+    if (lane < kCullTS) tile[lane] = cur;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll 8
     for (int kk = 0; kk < kCullTS; ++kk) {

@@ -15,11 +15,15 @@ dev = torch.device("cuda:0")
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 shapes = [tuple(int(v) for v in s.split("x")) for s in sys.argv[2:]] or [(16384, 16384)]
 tag = f"{os.environ.get('PCOPS_LIB_PATH', 'default')} Q={os.environ.get('PCOPS_CHAMFER_Q', 'auto')} " \
-      f"screen={os.environ.get('PCOPS_CHAMFER_SCREEN', '1')}"
+      f"screen={os.environ.get('PCOPS_CHAMFER_SCREEN', '1')} cull={os.environ.get('PCOPS_CHAMFER_CULL', '1')} " \
+      f"data={os.environ.get('CH_DATA', 'gauss')}"
 for N, M in shapes:
     g = torch.Generator(device="cpu").manual_seed(N + M)
     a = (torch.randn(32, N, 3, generator=g) * 0.45).to(dev)
     b = (torch.randn(32, M, 3, generator=g) * 0.45).to(dev)
+    if os.environ.get("CH_DATA") == "surface":  # ellipsoid surfaces (completion-like clouds)
+        a = (a / a.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
+        b = (b / b.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
     for _ in range(3):
         chamfer_3DDist()(a, b)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
