@@ -876,8 +876,11 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
   };
 
   float4 *tile = tiles[w];
+  // pass 1: per query the smallest distance (v_min chain, the NN kernels' 7 VALU / pair), the
+  // tile holding it, and whether another scanned tile reached the same minimum
   float best = INFINITY;
-  int bidx = INT_MAX;
+  int btile = 0;
+  bool tie = false;
   float mb = INFINITY;  // the wave's largest current best (scalar)
   float m;
   int t;
@@ -901,17 +904,43 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
     __builtin_amdgcn_wave_barrier();
     if (lane < kCullTS) tile[lane] = cur;
     __builtin_amdgcn_wave_barrier();
-#pragma unroll 8
-    for (int kk = 0; kk < kCullTS; ++kk) {
-      const float4 p = tile[kk];
-      const float d = sqd3(p.x - a.x, p.y - a.y, p.z - a.z);
-      const int ti = __float_as_int(p.w);
-      if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
+    float mt = INFINITY;
+#pragma unroll 2
+    for (int kk = 0; kk < kCullTS; kk += 2) {
+      const float4 p0 = tile[kk], p1 = tile[kk + 1];
+      mt = fminf(fminf(mt, sqd3(p0.x - a.x, p0.y - a.y, p0.z - a.z)), sqd3(p1.x - a.x, p1.y - a.y, p1.z - a.z));
     }
+    if (mt < best)
+      best = mt, btile = tc, tie = false;
+    else if (mt == best)
+      tie = true;
     mb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_f32(valid ? best : -INFINITY))));
   }
   if (!valid) return;
-  if (nanst || !finite3(a.x, a.y, a.z)) ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
+  int bidx = INT_MAX;
+  if (nanst || !finite3(a.x, a.y, a.z)) {
+    ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
+  } else {
+    // pass 2, the exact (distance, original index) winner: the best tile alone, or -- when
+    // another tile tied -- every tile whose box is within the best (the culling test above)
+    const float bound = best;
+    best = INFINITY;
+    for (int u = tie ? 0 : btile, ue = tie ? nt : btile + 1; u < ue; ++u) {
+      if (tie && !bad) {
+        const float4 l = blo[u], h = bhi[u];
+        const float px = fmaxf(0.f, fmaxf(l.x - a.x, a.x - h.x)), py = fmaxf(0.f, fmaxf(l.y - a.y, a.y - h.y)),
+                    pz = fmaxf(0.f, fmaxf(l.z - a.z, a.z - h.z));
+        const float pl = ((px * px + py * py) + pz * pz) * (1.f - 64.f * kU);
+        if (pl > bound && pl > 1e-30f) continue;
+      }
+      for (int k = u * kCullTS, ke = min(NT, k + kCullTS); k < ke; ++k) {
+        const float4 p = T[k];
+        const float d = sqd3(p.x - a.x, p.y - a.y, p.z - a.z);
+        const int ti = __float_as_int(p.w);
+        if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
+      }
+    }
+  }
   if (bidx == INT_MAX) bidx = 0;
   const int oq = __float_as_int(a.w);
   dist[oq] = best;
