@@ -187,7 +187,7 @@ def kernel_work(name, a):
     if name == "furthest_point_sampling":
         B, N, M = a[1], a[2], a[3]
         return 16.0 * B * N * M, "GB/s", HBM_PEAK, "hbm"
-    if name == "chamfer_3D.forward":
+    if name == "chamfer_3D.forward":  # all-pairs equivalent (the culled search evaluates a fraction of them)
         B, N, M = a[2], a[3], a[4]
         return 8.0 * 2 * B * N * M, "TFLOP/s", VALU_F32_PEAK, "valu"
     if name == "knn":
@@ -286,7 +286,7 @@ def kernel_work(name, a):
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
             "attention bwd": "attn_(delta2|dkv3|dqs)_kernel",
             "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
-            "chamfer_3D.forward": "chamfer_(nn|screen|mfma)_kernel", "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
+            "chamfer_3D.forward": (r"chamfer_(nn|screen|mfma|cull|cull_prep)_kernel", r"chamfer_(nn|screen|mfma|cull)_kernel"), "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
             "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",
             "colsum": ("colsum", "colsum_partial"),
             "transpose_add": "transpose_add", "pcsa_forward": "pcsa_fwd", "pcsa_backward": "pcsa_bwd",
