@@ -803,6 +803,7 @@ __device__ __forceinline__ float box_gap(float qlo, float qhi, float tlo, float 
 // grid (blocks of dir 0 + blocks of dir 1, B), kCullQB threads: one sorted query per lane.  Each
 // wave is an independent searcher over its 64 queries (its own box, bounds, tile buffer and
 // skip decisions): no block barriers, and a 64-query box is ~4x tighter than a block's.
+template <bool ES>
 __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__restrict__ xyz1,
                                                                const float *__restrict__ xyz2, int N, int M,
                                                                CullWs ws, float *__restrict__ dist1,
@@ -876,21 +877,32 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
   };
 
   float4 *tile = tiles[w];
-  // pass 1: per query the smallest distance (v_min chain, the NN kernels' 7 VALU / pair), the
-  // tile holding it, and whether another scanned tile reached the same minimum
-  float best = INFINITY;
+  // pass 1.  ES = false: per query the smallest distance (the direct expression + v_min, 6.5 VALU
+  // per pair), the tile holding it and whether another scanned tile reached the same minimum.
+  // ES = true: chamfer_screen_kernel's screen over the visited tiles -- e = |t|^2 - 2a.t (3 fma +
+  // 1/2 v_min per pair), its rounding margin and <= kSlots candidate tiles per query -- with the
+  // upper bound U = min e + |a|^2 + slack on the direct best distance as the culling bound.
+  float best = INFINITY;  // ES = false: the best distance; ES = true: U
   int btile = 0;
   bool tie = false;
-  float mb = INFINITY;  // the wave's largest current best (scalar)
+  const float mx = -2.f * a.x, my = -2.f * a.y, mz = -2.f * a.z;
+  const float an = (a.x * a.x + a.y * a.y) + a.z * a.z, anorm = sqrtf(an);
+  float mine = INFINITY, slack = INFINITY, eps_t2 = 0.f;
+  float cm[kSlots];
+  int cs[kSlots];
+#pragma unroll
+  for (int c = 0; c < kSlots; ++c) cm[c] = INFINITY, cs[c] = -1;
+  bool over = bad || !(an < INFINITY);
+  float mb = INFINITY;  // the wave's largest current bound (scalar)
   float m;
   int t;
   take(m, t);
   float4 pf = fetch(m, t);
-  for (;;) {
+  for (; !(ES && bad);) {  // (a non-finite batch: every query re-derived below by a full scan)
     if (m == INFINITY) break;         // every tile taken
     if (m > mb && m > 1e-30f) break;  // every untaken tile lies beyond every query's best
     const int tc = t;
-    const float4 cur = pf;
+    float4 cur = pf;
     take(m, t);  // the next tile, its points in flight while this one is scanned
     pf = fetch(m, t);
     // per-query test against the tile's box: the tile is scanned only if some query may improve
@@ -900,45 +912,103 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
     const float pl = ((px * px + py * py) + pz * pz) * (1.f - 64.f * kU);
     const bool need = valid && (bad || !(pl > best) || pl <= 1e-30f);
     if (!__any(need)) continue;
+    if (ES) cur.w = (cur.x * cur.x + cur.y * cur.y) + cur.z * cur.z;  // |t|^2 (NaN padding stays NaN)
     // one wave: its LDS accesses complete in issue order, the wave barriers keep the compiler's
     __builtin_amdgcn_wave_barrier();
     if (lane < kCullTS) tile[lane] = cur;
     __builtin_amdgcn_wave_barrier();
     float mt = INFINITY;
+    if (ES) {
 #pragma unroll 2
-    for (int kk = 0; kk < kCullTS; kk += 2) {
-      const float4 p0 = tile[kk], p1 = tile[kk + 1];
-      mt = fminf(fminf(mt, sqd3(p0.x - a.x, p0.y - a.y, p0.z - a.z)), sqd3(p1.x - a.x, p1.y - a.y, p1.z - a.z));
+      for (int kk = 0; kk < kCullTS; kk += 2) {
+        const float4 p0 = tile[kk], p1 = tile[kk + 1];
+        const float e0 = __builtin_fmaf(mz, p0.z, __builtin_fmaf(my, p0.y, __builtin_fmaf(mx, p0.x, p0.w)));
+        const float e1 = __builtin_fmaf(mz, p1.z, __builtin_fmaf(my, p1.y, __builtin_fmaf(mx, p1.x, p1.w)));
+        mt = fminf(fminf(mt, e0), e1);
+      }
+      // Tm^2: running max over the visited tiles of their box's farthest corner
+      const float cx = fmaxf(fabsf(l.x), fabsf(h.x)), cy = fmaxf(fabsf(l.y), fabsf(h.y)),
+                  cz = fmaxf(fabsf(l.z), fabsf(h.z));
+      eps_t2 = fmaxf(eps_t2, ((cx * cx + cy * cy) + cz * cz) * (1.f + 8.f * kU));
+      const float tm = sqrtf(eps_t2);
+      const float eps = 16.f * kU * (eps_t2 + anorm * tm);
+      over = over || !(eps_t2 + 2.f * anorm * tm < 1e38f);  // near fp32 overflow: full re-derivation
+      slack = screen_slack(mine, an, eps);
+      if (mt <= mine + slack) {  // this tile may hold the argmin (the screen's keep / prune)
+        if (mt < mine) {
+          mine = mt;
+          slack = screen_slack(mine, an, eps);
+#pragma unroll
+          for (int c = 0; c < kSlots; ++c)
+            if (cs[c] >= 0 && cm[c] > mine + slack) cs[c] = -1;
+        }
+        bool placed = false;
+#pragma unroll
+        for (int c = 0; c < kSlots; ++c)
+          if (!placed && cs[c] < 0) cs[c] = tc, cm[c] = mt, placed = true;
+        over = over || !placed;
+      }
+      best = mine + an + slack;
+    } else {
+#pragma unroll 2
+      for (int kk = 0; kk < kCullTS; kk += 2) {
+        const float4 p0 = tile[kk], p1 = tile[kk + 1];
+        mt = fminf(fminf(mt, sqd3(p0.x - a.x, p0.y - a.y, p0.z - a.z)), sqd3(p1.x - a.x, p1.y - a.y, p1.z - a.z));
+      }
+      if (mt < best)
+        best = mt, btile = tc, tie = false;
+      else if (mt == best)
+        tie = true;
     }
-    if (mt < best)
-      best = mt, btile = tc, tie = false;
-    else if (mt == best)
-      tie = true;
     mb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_f32(valid ? best : -INFINITY))));
   }
   if (!valid) return;
   int bidx = INT_MAX;
-  if (nanst || !finite3(a.x, a.y, a.z)) {
-    ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
-  } else {
-    // pass 2, the exact (distance, original index) winner: the best tile alone, or -- when
-    // another tile tied -- every tile whose box is within the best (the culling test above)
-    const float bound = best;
+  auto scan_tile = [&](int u) {
+    for (int k = u * kCullTS, ke = min(NT, k + kCullTS); k < ke; ++k) {
+      const float4 p = T[k];
+      const float d = sqd3(p.x - a.x, p.y - a.y, p.z - a.z);
+      const int ti = __float_as_int(p.w);
+      if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
+    }
+  };
+  // every tile whose box is within `bound` (all of them in a non-finite batch)
+  auto scan_within = [&](float bound) {
     best = INFINITY;
-    for (int u = tie ? 0 : btile, ue = tie ? nt : btile + 1; u < ue; ++u) {
-      if (tie && !bad) {
+    bidx = INT_MAX;
+    for (int u = 0; u < nt; ++u) {
+      if (!bad) {
         const float4 l = blo[u], h = bhi[u];
         const float px = fmaxf(0.f, fmaxf(l.x - a.x, a.x - h.x)), py = fmaxf(0.f, fmaxf(l.y - a.y, a.y - h.y)),
                     pz = fmaxf(0.f, fmaxf(l.z - a.z, a.z - h.z));
         const float pl = ((px * px + py * py) + pz * pz) * (1.f - 64.f * kU);
         if (pl > bound && pl > 1e-30f) continue;
       }
-      for (int k = u * kCullTS, ke = min(NT, k + kCullTS); k < ke; ++k) {
-        const float4 p = T[k];
-        const float d = sqd3(p.x - a.x, p.y - a.y, p.z - a.z);
-        const int ti = __float_as_int(p.w);
-        if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
-      }
+      scan_tile(u);
+    }
+  };
+  if (nanst || !finite3(a.x, a.y, a.z)) {
+    ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
+  } else if (ES) {
+    // pass 2, the exact (distance, original index) winner: over the candidate tiles, or -- on
+    // slot overflow / non-finite data / overflow risk -- over every tile within U
+    const float bound = best;
+    best = INFINITY;
+    if (!over) {
+#pragma unroll
+      for (int c = 0; c < kSlots; ++c)
+        if (cs[c] >= 0) scan_tile(cs[c]);
+    }
+    if (over || !(best < INFINITY)) scan_within(bad ? INFINITY : bound);
+  } else {
+    // pass 2, the exact (distance, original index) winner: the best tile alone, or -- when
+    // another tile tied -- every tile whose box is within the best (the culling test above)
+    const float bound = best;
+    if (tie) {
+      scan_within(bound);
+    } else {
+      best = INFINITY;
+      scan_tile(btile);
     }
   }
   if (bidx == INT_MAX) bidx = 0;
@@ -994,14 +1064,15 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
     const char *e = getenv("PCOPS_CHAMFER_SCREEN");
     return !(e && e[0] == '0');
   }();
-  // PCOPS_CHAMFER_MFMA: 0 = the VALU screen only, 1 (default) = the MFMA screen for the launches
-  // the VALU screen runs at Q = 1 (B = 32, 2048^2: 0.071 -> 0.048 ms; PCN step 51.88 -> 51.58 ms,
-  // same box), 2 = everywhere: at 16384^2 alone it ties the Q = 4 VALU screen (1.67 vs 1.69 ms), in
-  // the step it measured 0.4-0.8 ms slower (it shares the matrix cores with the concurrent GEMMs /
-  // attention of the other stream); profiles/r3_chamfer_mfma_ab.txt
+  // PCOPS_CHAMFER_MFMA: 0 (default) = the VALU screen only -- the brief reserves the matrix cores
+  // for the attention contractions; 1 = the fp32-MFMA screen for the launches the VALU screen runs
+  // at Q = 1 (opt-in: B = 32, 2048^2: 0.071 -> 0.048 ms; PCN step 51.88 -> 51.58 ms, same box),
+  // 2 = everywhere: at 16384^2 alone it ties the Q = 4 VALU screen (1.67 vs 1.69 ms), in the step it
+  // measured 0.4-0.8 ms slower (it shares the matrix cores with the concurrent GEMMs / attention
+  // of the other stream); profiles/r3_chamfer_mfma_ab.txt
   const int mfma = [] {
     const char *e = getenv("PCOPS_CHAMFER_MFMA");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   if (screen && (mfma == 2 || (mfma == 1 && Q == 1))) {
     const int m0 = (N + kThreads / 2 - 1) / (kThreads / 2), m1 = (M + kThreads / 2 - 1) / (kThreads / 2);
@@ -1079,8 +1150,14 @@ extern "C" int pcops_chamfer_forward_ws(const float *xyz1, const float *xyz2, in
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(chamfer_cull_prep_kernel, dim3(B, 2), dim3(1024), 0, s, xyz1, xyz2, N, M, ws);
   const int b0 = (N + kCullQB - 1) / kCullQB, b1 = (M + kCullQB - 1) / kCullQB;
-  hipLaunchKernelGGL(chamfer_cull_kernel, dim3(b0 + b1, B), dim3(kCullQB), 0, s, xyz1, xyz2, N, M, ws, dist1, dist2,
-                     idx1, idx2, b0);
+  // PCOPS_CHAMFER_CULL_ES=0: the direct-expression pass 1 (A/B)
+  const char *es = getenv("PCOPS_CHAMFER_CULL_ES");
+  if (es && es[0] == '0')
+    hipLaunchKernelGGL(chamfer_cull_kernel<false>, dim3(b0 + b1, B), dim3(kCullQB), 0, s, xyz1, xyz2, N, M, ws, dist1,
+                       dist2, idx1, idx2, b0);
+  else
+    hipLaunchKernelGGL(chamfer_cull_kernel<true>, dim3(b0 + b1, B), dim3(kCullQB), 0, s, xyz1, xyz2, N, M, ws, dist1,
+                       dist2, idx1, idx2, b0);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }

@@ -362,16 +362,20 @@ def _screen_clouds(kind, rng):
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("q", ["2", "4"])
+@pytest.mark.parametrize("q", ["1", "2", "4", "mfma"])
 @pytest.mark.parametrize("kind", ["uniform", "tiled", "outliers", "offset", "nonfinite"])
 def test_chamfer_screen_bitexact(dev, monkeypatch, kind, q):
-    """The screened kernel (e = |t|^2 - 2a.t ranks sub-tiles, the reference
+    """The screened kernels (e = |t|^2 - 2a.t ranks sub-tiles, the reference
     expression re-derives the winner) forced onto small clouds through
-    PCOPS_CHAMFER_Q: bit-exact distances and indices against the oracle on
-    exact ties, far outliers, a cloud far from the origin and non-finite points."""
+    PCOPS_CHAMFER_Q (VALU screen) / PCOPS_CHAMFER_MFMA=2 (the opt-in fp32-MFMA screen):
+    bit-exact distances and indices against the oracle on exact ties, far outliers, a
+    cloud far from the origin and non-finite points."""
     from svdformer_pointsea_amd.chamfer3D import chamfer_3DDist
 
-    monkeypatch.setenv("PCOPS_CHAMFER_Q", q)
+    if q == "mfma":
+        monkeypatch.setenv("PCOPS_CHAMFER_MFMA", "2")
+    else:
+        monkeypatch.setenv("PCOPS_CHAMFER_Q", q)
     a, b = _screen_clouds(kind, np.random.default_rng(len(kind) * 7 + int(q)))
     got = [t.cpu().numpy() for t in chamfer_3DDist()(T(a, dev), T(b, dev))]
     ref = O.chamfer_forward(a, b)
@@ -380,7 +384,8 @@ def test_chamfer_screen_bitexact(dev, monkeypatch, kind, q):
 
 
 @pytest.mark.parametrize("kernel", [{}, {"PCOPS_CHAMFER_Q": "2"}, {"PCOPS_CHAMFER_Q": "4"},
-                                    {"PCOPS_CHAMFER_SCREEN": "0"}, {"PCOPS_CHAMFER_Q": "4", "PCOPS_CHAMFER_MFMA": "2"}])
+                                    {"PCOPS_CHAMFER_SCREEN": "0"}, {"PCOPS_CHAMFER_MFMA": "1"},
+                                    {"PCOPS_CHAMFER_Q": "4", "PCOPS_CHAMFER_MFMA": "2"}])
 def test_chamfer_nonfinite_scan_order(dev, monkeypatch, kernel):
     """The reference's chunked scan order on non-finite data (chamfer3D.cu:16-129), every
     forward kernel (MFMA screen, VALU screen Q=2/4, direct) against the oracle, bitwise: a NaN
