@@ -688,7 +688,10 @@ __global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
 // so a skipped tile holds no pair at or below the best; below 1e-30 nothing is skipped
 // (denormal scale).  A cloud with a non-finite coordinate disables the culling for its batch
 // (every tile scanned) and sends the queries ref_scan covers there.
-constexpr int kCullQB = 256, kCullTS = 32, kCullMaxTiles = 512, kCellBits = 4, kCells = 1 << (3 * kCellBits);
+#ifndef PCOPS_CULL_TS
+#define PCOPS_CULL_TS 32  // A/B builds: -DPCOPS_CULL_TS=64
+#endif
+constexpr int kCullQB = 256, kCullTS = PCOPS_CULL_TS, kCullMaxTiles = 512, kCellBits = 4, kCells = 1 << (3 * kCellBits);
 
 __device__ __forceinline__ int cull_cell(float x, float y, float z, const float *g) {
   auto ax = [](float v, float lo, float sc) {
