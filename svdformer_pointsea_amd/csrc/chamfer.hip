@@ -689,7 +689,7 @@ __global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
 // (denormal scale).  A cloud with a non-finite coordinate disables the culling for its batch
 // (every tile scanned) and sends the queries ref_scan covers there.
 #ifndef PCOPS_CULL_TS
-#define PCOPS_CULL_TS 32  // A/B builds: -DPCOPS_CULL_TS=64
+#define PCOPS_CULL_TS 64  // A/B builds: -DPCOPS_CULL_TS=32 (one point per lane: <= 64)
 #endif
 constexpr int kCullQB = 256, kCullTS = PCOPS_CULL_TS, kCullMaxTiles = 512, kCellBits = 4, kCells = 1 << (3 * kCellBits);
 
