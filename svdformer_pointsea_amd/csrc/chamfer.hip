@@ -935,7 +935,8 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
       eps_t2 = fmaxf(eps_t2, ((cx * cx + cy * cy) + cz * cz) * (1.f + 8.f * kU));
       const float tm = sqrtf(eps_t2);
       const float eps = 16.f * kU * (eps_t2 + anorm * tm);
-      over = over || !(eps_t2 + 2.f * anorm * tm < 1e38f);  // near fp32 overflow: full re-derivation
+      const bool ovf = !(eps_t2 + 2.f * anorm * tm < 1e38f);  // near fp32 overflow: e may be +-inf / NaN
+      over = over || ovf;                                      // -> full re-derivation, no culling
       slack = screen_slack(mine, an, eps);
       if (mt <= mine + slack) {  // this tile may hold the argmin (the screen's keep / prune)
         if (mt < mine) {
@@ -952,6 +953,7 @@ __global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__re
         over = over || !placed;
       }
       best = mine + an + slack;
+      if (ovf || !(best >= 0.f)) best = INFINITY;  // no valid bound: this query culls nothing
     } else {
 #pragma unroll 2
       for (int kk = 0; kk < kCullTS; kk += 2) {

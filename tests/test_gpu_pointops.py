@@ -690,7 +690,7 @@ def test_knn3_adversarial_bitexact(dev, monkeypatch, B, S, N, K, pad, kind):
 @pytest.mark.parametrize("B,N,M,kind", [(2, 16384, 16384, "gauss"), (3, 16384, 8192, "surface"),
                                         (2, 8192, 8192, "dup"), (2, 4096, 16000, "clusters"),
                                         (3, 6000, 5000, "nonfinite"), (2, 4096, 4096, "same"),
-                                        (2, 5000, 7000, "huge"), (2, 4096, 4100, "tiny"), (32, 16384, 16384, "pcn")])
+                                        (2, 5000, 7000, "huge"), (2, 4096, 6000, "huge2"), (2, 4096, 4100, "tiny"), (32, 16384, 16384, "pcn")])
 def test_chamfer_culled_bitexact(dev, B, N, M, kind):
     """The spatially culled Chamfer search (pcops_chamfer_forward_ws: Morton-sorted clouds, tile
     boxes, blocks skipping tiles beyond their current best under a rigorous margin) against the
@@ -729,6 +729,9 @@ def test_chamfer_culled_bitexact(dev, B, N, M, kind):
         b = torch.full((B, M, 3), 0.25)
     elif kind == "huge":
         a, b = torch.randn(B, N, 3, generator=g) * 1e19, torch.randn(B, M, 3, generator=g) * 1e19
+    elif kind == "huge2":  # |t|^2 and 2 a.t overflow fp32: the screens' e is +-inf / NaN
+        a, b = torch.randn(B, N, 3, generator=g) * 4e19, torch.randn(B, M, 3, generator=g) * 4e19
+        a[:, ::3] *= 1e-10  # and some queries small enough for finite distances
     else:
         a, b = torch.randn(B, N, 3, generator=g) * 1e-20, torch.randn(B, M, 3, generator=g) * 1e-20
     a, b = a.float().contiguous().to(dev), b.float().contiguous().to(dev)
@@ -749,6 +752,6 @@ def test_chamfer_culled_bitexact(dev, B, N, M, kind):
         outs.append((d1, d2, i1, i2))
     for x, y in zip(*outs):
         np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
-    if kind in ("nonfinite", "huge", "tiny"):  # and against the oracle
+    if kind in ("nonfinite", "huge", "huge2", "tiny"):  # and against the oracle
         for x, y in zip(outs[1], O.chamfer_forward(a.cpu().numpy(), b.cpu().numpy())):
             np.testing.assert_array_equal(x.cpu().numpy(), y)
