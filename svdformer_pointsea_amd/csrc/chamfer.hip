@@ -806,8 +806,11 @@ __device__ __forceinline__ float box_gap(float qlo, float qhi, float tlo, float 
 // grid (blocks of dir 0 + blocks of dir 1, B), kCullQB threads: one sorted query per lane.  Each
 // wave is an independent searcher over its 64 queries (its own box, bounds, tile buffer and
 // skip decisions): no block barriers, and a 64-query box is ~4x tighter than a block's.
+#ifndef PCOPS_CULL_WPE
+#define PCOPS_CULL_WPE 1  // A/B builds: -DPCOPS_CULL_WPE=8 (occupancy hint)
+#endif
 template <bool ES>
-__global__ __launch_bounds__(kCullQB) void chamfer_cull_kernel(const float *__restrict__ xyz1,
+__global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_CULL_WPE))) void chamfer_cull_kernel(const float *__restrict__ xyz1,
                                                                const float *__restrict__ xyz2, int N, int M,
                                                                CullWs ws, float *__restrict__ dist1,
                                                                float *__restrict__ dist2, int *__restrict__ idx1,
