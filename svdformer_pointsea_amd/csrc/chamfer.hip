@@ -807,7 +807,7 @@ __device__ __forceinline__ float box_gap(float qlo, float qhi, float tlo, float 
 // wave is an independent searcher over its 64 queries (its own box, bounds, tile buffer and
 // skip decisions): no block barriers, and a 64-query box is ~4x tighter than a block's.
 #ifndef PCOPS_CULL_WPE
-#define PCOPS_CULL_WPE 1  // A/B builds: -DPCOPS_CULL_WPE=8 (occupancy hint)
+#define PCOPS_CULL_WPE 7  // occupancy hint: 72 VGPRs, 7 waves / SIMD (LDS allows 7 blocks / CU); A/B builds override
 #endif
 template <bool ES>
 __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_CULL_WPE))) void chamfer_cull_kernel(const float *__restrict__ xyz1,
