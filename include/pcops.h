@@ -145,10 +145,11 @@ int pcops_knn_ws(const float *q, const float *p, int B, int S, int N, int C, int
 int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B, int N, int M, float *dist1, float *dist2,
                           int *idx1, int *idx2, pcops_stream_t stream);
 /* pcops_chamfer_forward_ws: pcops_chamfer_forward through a spatially culled search for large clouds
- *   (N, M >= 4096, <= 65536): both clouds counting-sorted by a 16^3 Morton cell code, targets in
- *   64-point tiles with exact boxes, each 256-query block scanning only the tiles its box can reach
- *   under a rigorous fp32 margin; the reference's distance bits and lowest-index tie rule, including
- *   its non-finite behaviour (culling off for a batch holding a non-finite coordinate).  workspace:
+ *   (4096 <= N, M <= 32768): both clouds counting-sorted by a 16^3 Morton cell code, targets in
+ *   64-point tiles with exact boxes, each wave (64 sorted queries) taking tiles nearest-first and
+ *   skipping every tile beyond its queries' bounds under a rigorous fp32 margin; the reference's
+ *   distance bits and lowest-index tie rule, including its non-finite behaviour (culling off for a
+ *   batch holding a non-finite coordinate).  workspace:
  *   pcops_chamfer_workspace_bytes (0: the sizes take pcops_chamfer_forward, as does a short
  *   workspace).  Replaces the same call as pcops_chamfer_forward (chamfer_cuda.cpp:17-24). */
 unsigned long long pcops_chamfer_workspace_bytes(int B, int N, int M);

@@ -12,7 +12,10 @@
 //                          re-derived from the winning sub-tile (7 VALU / pair);
 //   chamfer_screen_kernel  ranks targets by |t|^2 - 2 a.t (3.5 VALU / pair) under
 //                          a rigorous rounding margin and re-derives the winner
-//                          with the direct expression (see its comment).
+//                          with the direct expression (see its comment);
+//   chamfer_mfma_kernel    the same screen on fp32 MFMA (opt-in, PCOPS_CHAMFER_MFMA).
+// Large clouds go through pcops_chamfer_forward_ws instead: Morton-sorted clouds and a
+// culled, nearest-first search per wave over 64-point tiles (the last section).
 //
 // Backward (chamfer3D.cu:155-195: own and partner terms both by float
 // atomics, so its sums depend on arrival order): one launch in which every
@@ -159,7 +162,6 @@ __global__ __launch_bounds__(kThreads) void chamfer_nn_kernel(const float *__res
         break;
       }
     }
-    if (!(best[i] == best[i])) bk = 0;  // NaN query: reference keeps its first candidate
     dist[qi] = best[i] < INFINITY ? best[i] : sqd3(T[3 * bk] - ax[i], T[3 * bk + 1] - ay[i], T[3 * bk + 2] - az[i]);
     idx[qi] = bk;
   }
