@@ -1,16 +1,6 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r4wpe; mkdir -p $O
+O=gpurun_out/r4fin3; mkdir -p $O
 export TMPDIR=/tmp
-L=$PWD/ablc/wpe7/libpcops.so
-PCOPS_LIB_PATH=$L PYTEST_K="culled" bash tools/gpu_run.sh $O/wpe7 tests_k || exit 1
-for d in gauss surface; do
-  CH_DATA=$d timeout -k 10 120 python tools/chamfer_bench.py 20 16384x16384 8192x8192 >> $O/ch_base.txt 2>&1 || exit 1
-  PCOPS_LIB_PATH=$L CH_DATA=$d timeout -k 10 120 python tools/chamfer_bench.py 20 16384x16384 8192x8192 >> $O/ch_wpe7.txt 2>&1 || exit 1
-done
-B="--no-cpu-baseline --no-fp32-leg --no-extra-legs"
-for i in 1 2; do
-  timeout -k 10 300 python bench.py $B > $O/pcn_base_$i.json 2> $O/pcn_base_$i.err || exit 1
-  PCOPS_LIB_PATH=$L timeout -k 10 300 python bench.py $B > $O/pcn_wpe7_$i.json 2> $O/pcn_wpe7_$i.err || exit 1
-done
+bash tools/gpu_run.sh $O tests smoke trace bench || exit 1
