@@ -6,6 +6,7 @@ all-reduce after backward, bitwise, on the bf16-shadow + fp32 parameter
 layout bench.py uses."""
 import copy
 import socket
+import time
 
 import pytest
 import torch
@@ -100,8 +101,13 @@ def test_bucketed_allreduce_rccl(dev, group, graph, bucket_mb):
     torch.cuda.synchronize()
     assert torch.equal(fb.grad, ref)
     if graph:
+        # as bench.py captures its collectives: RCCL's watchdog thread polls the eager
+        # collectives' events, and under "global" capture such a call from another thread
+        # invalidates the capture (the watchdog then aborts the process) -- so drain, let it
+        # finish polling, and capture in thread-local mode
+        time.sleep(1.0)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             _step(fb, x, sync)
         fb.grad.fill_(float("nan"))
         g.replay()
