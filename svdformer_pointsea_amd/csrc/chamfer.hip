@@ -1039,7 +1039,11 @@ bool cull_applies(int N, int M) {
     const char *e = getenv("PCOPS_CHAMFER_CULL");
     return !(e && e[0] == '0');
   }();
-  return on && N >= 4096 && M >= 4096 && (N + kCullTS - 1) / kCullTS <= kCullMaxTiles &&
+  static const int lo = [] {  // PCOPS_CHAMFER_CULL_MIN: smallest cloud culled (A/B)
+    const char *e = getenv("PCOPS_CHAMFER_CULL_MIN");
+    return e ? atoi(e) : 4096;
+  }();
+  return on && N >= lo && M >= lo && (N + kCullTS - 1) / kCullTS <= kCullMaxTiles &&
          (M + kCullTS - 1) / kCullTS <= kCullMaxTiles;
 }
 
