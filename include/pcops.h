@@ -131,10 +131,10 @@ int pcops_three_interpolate_grad(const float *grad_out, const int *idx, const fl
  * idx (B,S,K) int32; dist (B,S,K) optional (may be NULL).  C <= 512, K+pad <= 64. */
 int pcops_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
               pcops_stream_t stream);
-/* The same with scratch (pcops_knn_workspace_bytes; 0 = none needed): for C == 3, K + pad <= 16,
- * S and N <= 4096 both clouds are sorted by Morton code first and each block of 64 spatially
- * adjacent queries scans the candidates nearest-first -- the same output bit for bit (every
- * candidate is still compared, as a (distance, index) pair); otherwise pcops_knn. */
+/* The same with scratch (pcops_knn_workspace_bytes(B, S, N, C, K + pad); 0 = none needed): a
+ * feature-space search (C >= 32, C % 4 == 0, K + pad <= 32) streams the candidates split over
+ * blocks (knnC3_kernel) and merges the partial sorted lists as (distance, index) pairs -- the same
+ * output bit for bit; every other case, or a short workspace, is pcops_knn. */
 unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int C, int K);
 int pcops_knn_ws(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx, float *dist,
                  void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
@@ -145,7 +145,7 @@ int pcops_knn_ws(const float *q, const float *p, int B, int S, int N, int C, int
 int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B, int N, int M, float *dist1, float *dist2,
                           int *idx1, int *idx2, pcops_stream_t stream);
 /* pcops_chamfer_forward_ws: pcops_chamfer_forward through a spatially culled search for large clouds
- *   (4096 <= N, M <= 32768): both clouds counting-sorted by a 16^3 Morton cell code, targets in
+ *   (N, M >= 256, N * M >= 2^24, both <= 32768): both clouds counting-sorted by a 16^3 Morton cell code, targets in
  *   64-point tiles with exact boxes, each wave (64 sorted queries) taking tiles nearest-first and
  *   skipping every tile beyond its queries' bounds under a rigorous fp32 margin; the reference's
  *   distance bits and lowest-index tie rule, including its non-finite behaviour (culling off for a
