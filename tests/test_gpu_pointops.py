@@ -690,7 +690,8 @@ def test_knn3_adversarial_bitexact(dev, monkeypatch, B, S, N, K, pad, kind):
 @pytest.mark.parametrize("B,N,M,kind", [(2, 16384, 16384, "gauss"), (3, 16384, 8192, "surface"),
                                         (2, 8192, 8192, "dup"), (2, 4096, 16000, "clusters"),
                                         (3, 6000, 5000, "nonfinite"), (2, 4096, 4096, "same"),
-                                        (2, 5000, 7000, "huge"), (2, 4096, 6000, "huge2"), (2, 4096, 4100, "tiny"), (32, 16384, 16384, "pcn")])
+                                        (2, 5000, 7000, "huge"), (2, 4096, 6000, "huge2"), (2, 4096, 4100, "tiny"), (3, 1024, 16384, "surface"),
+                                        (2, 16384, 2048, "gauss"), (32, 16384, 16384, "pcn")])
 def test_chamfer_culled_bitexact(dev, B, N, M, kind):
     """The spatially culled Chamfer search (pcops_chamfer_forward_ws: Morton-sorted clouds, tile
     boxes, blocks skipping tiles beyond their current best under a rigorous margin) against the
