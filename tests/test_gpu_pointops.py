@@ -694,7 +694,8 @@ def test_knn3_adversarial_bitexact(dev, monkeypatch, B, S, N, K, pad, kind):
                                         (2, 16384, 2048, "gauss"), (32, 16384, 16384, "pcn")])
 def test_chamfer_culled_bitexact(dev, B, N, M, kind):
     """The spatially culled Chamfer search (pcops_chamfer_forward_ws: Morton-sorted clouds, tile
-    boxes, blocks skipping tiles beyond their current best under a rigorous margin) against the
+    boxes, waves taking tiles nearest-first and skipping those beyond their queries' bounds under a
+    rigorous margin) against the
     all-pairs screens (pcops_chamfer_forward): dist and idx bitwise, both directions.  Exact
     duplicates (ties across tiles), far clusters, NaN / inf points (culling off, the reference's
     first-candidate rule), a single repeated point, coordinates whose squares overflow, and
