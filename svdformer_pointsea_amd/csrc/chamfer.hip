@@ -1046,7 +1046,11 @@ bool cull_applies(int N, int M) {
     const char *e = getenv("PCOPS_CHAMFER_CULL_MIN");
     return e ? atoi(e) : 256;
   }();
-  return on && N >= lo && M >= lo && (long long)N * M >= (1LL << 24) && (N + kCullTS - 1) / kCullTS <= kCullMaxTiles &&
+  static const long long pairs = [] {  // PCOPS_CHAMFER_CULL_PAIRS: smallest N * M culled (A/B)
+    const char *e = getenv("PCOPS_CHAMFER_CULL_PAIRS");
+    return e ? atoll(e) : (1LL << 24);
+  }();
+  return on && N >= lo && M >= lo && (long long)N * M >= pairs && (N + kCullTS - 1) / kCullTS <= kCullMaxTiles &&
          (M + kCullTS - 1) / kCullTS <= kCullMaxTiles;
 }
 
