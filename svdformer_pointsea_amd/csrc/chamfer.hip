@@ -820,9 +820,15 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
   constexpr int W = kCullQB / 64, kLbRegs = kCullMaxTiles / 64;
   __shared__ float4 tiles[W][kCullTS];
   __shared__ float4 blo[kCullMaxTiles], bhi[kCullMaxTiles];  // the target tiles' boxes
-  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int dir = (int)blockIdx.x >= blocks_dir0;
-  const int bx = dir ? blockIdx.x - blocks_dir0 : blockIdx.x;
+  // XCD-contiguous (as chamfer_grad_seg_kernel): hardware block h runs on XCD h % 8, so the
+  // logical blocks of a (batch, direction) -- which all read the same sorted target cloud and
+  // write the same output rows -- are gathered onto one XCD and its L2
+  const int gx = (int)gridDim.x, total = gx * (int)gridDim.y;
+  int lin = (int)blockIdx.x + (int)blockIdx.y * gx;
+  if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
+  const int b = lin / gx, bxl = lin - b * gx, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dir = bxl >= blocks_dir0;
+  const int bx = dir ? bxl - blocks_dir0 : bxl;
   const int NA = dir ? M : N, NT = dir ? N : M;
   const float4 *A = ws.srt[dir] + (size_t)b * NA;
   const float4 *T = ws.srt[1 - dir] + (size_t)b * NT;
