@@ -82,6 +82,8 @@ def parse():
                          "the headline (N = 1 only)")
     ap.add_argument("--dry-run-launch", action="store_true",
                     help="with --gpus N > 1 outside torch.distributed.run: print the rank launcher's argv and exit")
+    ap.add_argument("--pmc-attn-json", default=os.path.join(ROOT, "profiles", "r4_pmc_attn.json"),
+                    help="attention MFMA counters (tools/pmc_attn.py) -> attention.pmc_mfma_util")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r4_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
@@ -285,7 +287,7 @@ def kernel_work(name, a):
 # libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
             "attention bwd": "attn_(delta2|dkv3|dqs)_kernel",
-            "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream)_kernel",
+            "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream|wave)_kernel",
             "chamfer_3D.forward": (r"chamfer_(nn|screen|mfma|cull|cull_prep)_kernel", r"chamfer_(nn|screen|mfma|cull)_kernel"), "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
             "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",
             "colsum": ("colsum", "colsum_partial"),
@@ -361,6 +363,17 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
     call group), `fps_us_per_round`, `composite_fps_knn_chamfer` and the per-call
     `kernels` table (HIP-event times per step, frac, PMC traffic ratio)."""
     out = {}
+
+    def pmc_row(k, r):
+        t = pmc_traffic(pmc_json, k, r["name"])
+        if t is None or not r["launches"] or r["ms"] <= 0:
+            return {}
+        # measured HBM bandwidth: PMC bytes per launch / this run's HIP-event launch time
+        row = {"pmc_bytes_per_launch": round(t), "pmc_gbs": round(t / (r["ms"] / r["launches"] * 1e-3) / 1e9, 2)}
+        if r.get("work") and r.get("unit") == "GB/s":
+            row["pmc_traffic_ratio"] = round(t / (r["work"] / r["launches"]), 3)
+        return row
+
     timed = {k: r for k, r in rows.items() if "frac" in r}
     if not timed:
         return out
@@ -372,6 +385,7 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
                        "traffic": pmc_traffic(pmc_json, dom_key, d["name"]),
                        "traffic_source": os.path.relpath(pmc_json, ROOT) if pmc_json else None,
                        "avg_launch_ms": round(d["ms"] / d["launches"], 4),
+                       **{k2: v for k2, v in pmc_row(dom_key, d).items() if k2 == "pmc_gbs"},
                        "work_per_launch": d["work"] / d["launches"]}
     # FPS is M-1 serially dependent rounds: its honest figure is time per round
     fps = {}
@@ -384,11 +398,36 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
     if group:
         out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) / sum(r["ms"] for r in group), 4)
 
-    def pmc_row(k, r):
-        t = pmc_traffic(pmc_json, k, r["name"])
-        if t is None or not r.get("work") or r.get("unit") != "GB/s":
-            return {}
-        return {"pmc_traffic_ratio": round(t / (r["work"] / r["launches"]), 3)}
+    # SURVEY 8(d)'s three north_star kernel groups side by side: the algorithmic model rate and frac
+    # next to the rocprof-measured HBM bandwidth (PMC bytes / launch time) -- FPS keeps its cloud on
+    # chip, so its measured GB/s is small by design; kNN and Chamfer are VALU-bound
+    out["north_star_kernels"] = {}
+    for k in ("furthest_point_sampling", "knn", "chamfer_3D.forward"):
+        r = rows.get(k)
+        if r is None or "frac" not in r:
+            continue
+        out["north_star_kernels"][k] = {"ms_per_step": round(r["ms"] / span_steps, 4),
+                                        "model_achieved": round(r["achieved"], 2), "model_unit": r["unit"],
+                                        "model_frac": round(r["frac"], 4), **pmc_row(k, r)}
+
+    # attention as ONE figure: credited FLOPs of every attention call / their summed launch time,
+    # and the time-weighted MFMA utilisation of the attention kernels from a rocprofv3 --pmc pass
+    # (tools/pmc_attn.py: SQ_VALU_MFMA_BUSY_CYCLES / (cycles x SIMDs))
+    att = [r for r in timed.values() if r["name"] in ATTN_ARGS and r["unit"] == "TFLOP/s"]
+    if att:
+        w, ms = sum(r["work"] for r in att), sum(r["ms"] for r in att)
+        peak = max(r["peak"] for r in att)
+        agg = {"ms_per_step": round(ms / span_steps, 4), "achieved_tflops": round(w / (ms * 1e-3) / 1e12, 2),
+               "peak_tflops": peak / 1e12, "frac": round(w / (ms * 1e-3) / peak, 4)}
+        pa = getattr(kernel_summary, "pmc_attn_json", None)
+        if pa and os.path.exists(pa):
+            tab = json.load(open(pa))
+            tw = sum(v["avg_us"] * v["launches"] for v in tab.values() if "mfma_util" in v)
+            if tw > 0:
+                agg["pmc_mfma_util"] = round(sum(v["mfma_util"] * v["avg_us"] * v["launches"]
+                                                 for v in tab.values() if "mfma_util" in v) / tw, 4)
+                agg["pmc_source"] = os.path.relpath(pa, ROOT)
+        out["attention"] = agg
 
     out["kernels"] = {k: {"launches_per_step": r["launches"] / span_steps,
                           "ms_per_step": round(r["ms"] / span_steps, 4),
@@ -749,7 +788,10 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
         if not math.isfinite(v):
             names = [n for n, q in model.named_parameters() if not torch.isfinite(q.detach()).all()]
             progress(f"[{tag}] non-finite running loss after {what}; master finite "
-                     f"{bool(torch.isfinite(fp.flat).all())}, grad finite {bool(torch.isfinite(fp.grad).all())}; "
+                     f"{bool(torch.isfinite(fp.flat).all())}, grad finite {bool(torch.isfinite(fp.grad[fp.n16:]).all())}"
+                     # with FlatAdam the shadow region's gradients live in grad16 only (collect(widen=False))
+                     f" / {bool(torch.isfinite(fp.grad16 if fopt is not None and not use_dist else fp.grad[:fp.n16]).all())}"
+                     f" (fp32 / shadow region); "
                      f"{len(names)} parameters non-finite, first: {names[:6]}")
             raise RuntimeError(f"non-finite loss ({tag}, {what})")
 
@@ -914,6 +956,7 @@ def extra_leg(args, name, batch, amp, device, steps):
 def main():
     global _RESULT_FD
     args = parse()
+    kernel_summary.pmc_attn_json = args.pmc_attn_json
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N`: one rank per GPU, started before anything touches the GPU
         sys.exit(self_launch(args))

@@ -768,10 +768,21 @@ int launch_knnC3(const float *q, const float *p, int B, int S, int N, int C, int
   return PCOPS_OK;
 }
 
+bool knnC3_on() {  // PCOPS_KNN_C3=0: knnC2_kernel (A/B)
+  static const bool v = [] {
+    const char *e = getenv("PCOPS_KNN_C3");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// the one predicate for the streamed, candidate-split form: the size query and the call agree, so
+// a caller never grows scratch that the call would not use (kk = K + pad)
+bool knnC3_eligible(int C, int kk) { return knnC3_on() && C >= 32 && C <= 512 && (C & 3) == 0 && kk <= 32 && !knn_v1(); }
+
 extern "C" unsigned long long pcops_knn_workspace_bytes(int B, int S, int N, int C, int K) {
   if (B <= 0 || S <= 0 || N <= 0 || C <= 0 || K <= 0) return 0;
-  if (C >= 32 && C <= 512 && K <= 32) return knnC3_bytes(B, S, N, K);
-  return 0;
+  return knnC3_eligible(C, K) ? knnC3_bytes(B, S, N, K) : 0;
 }
 
 extern "C" int pcops_knn(const float *q, const float *p, int B, int S, int N, int C, int K, int pad, int *idx,
@@ -786,12 +797,8 @@ extern "C" int pcops_knn_ws(const float *q, const float *p, int B, int S, int N,
   if (B == 0 || S == 0 || K == 0) return PCOPS_OK;
   if (!q || !p || !idx || N <= 0) return PCOPS_ERR_INVALID;
   if (K + pad > N) return PCOPS_ERR_INVALID;
-  static const bool c3 = [] {  // PCOPS_KNN_C3=0: knnC2_kernel (A/B)
-    const char *e = getenv("PCOPS_KNN_C3");
-    return !(e && e[0] == '0');
-  }();
   const int kk = K + pad;
-  if (c3 && C >= 32 && (C & 3) == 0 && kk <= 32 && workspace && workspace_bytes >= knnC3_bytes(B, S, N, kk) && !knn_v1()) {
+  if (knnC3_eligible(C, kk) && workspace && workspace_bytes >= knnC3_bytes(B, S, N, kk)) {
     hipStream_t st = (hipStream_t)stream;
     switch (kk_of(kk)) {
       case 4: return launch_knnC3<4>(q, p, B, S, N, C, K, pad, idx, dist, workspace, st);

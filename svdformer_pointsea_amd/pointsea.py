@@ -37,6 +37,8 @@ from .batchnorm import ACT_RELU, bn_act
 from .pointnet2_utils import furthest_point_sample, gather_operation
 from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin
 
+_LOCAL_FPS_FORK = os.environ.get("PCOPS_LOCAL_FPS_FORK", "0") == "1"
+
 
 # PCOPS_PS_CAT16=0: the path-selection concatenation in fp32, cast by autocast (A/B)
 _CAT16 = os.environ.get("PCOPS_PS_CAT16", "1") != "0"
@@ -216,8 +218,16 @@ class local_encoder(nn.Module):
         self.local_number = cfg.NETWORK.local_points
 
     def forward(self, inp):
-        x1 = self.gcn_1(inp)
-        idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
+        # the FPS depends on the input cloud only: PCOPS_LOCAL_FPS_FORK=1 runs it on a stream of its
+        # own (lane 3, nested in the model's lane-0 local-encoder fork) beside gcn_1
+        if _LOCAL_FPS_FORK:
+            with fork(inp.device, lane=3, inputs=(inp,)) as br:
+                idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
+            x1 = self.gcn_1(inp)
+            idx = br.join(idx)
+        else:
+            x1 = self.gcn_1(inp)
+            idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
         x1 = gather_operation(x1.float().contiguous(), idx)
         x2 = self.gcn_2(x1)
         x3 = self.gcn_3(x2)

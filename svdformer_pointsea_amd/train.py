@@ -73,6 +73,9 @@ class FlatParams:
         self.n_train = total - sum(p.numel() for n, p in named if n in frozen)
         self.frozen = frozen
         self.flat = torch.empty(total, dtype=torch.float32, device=device)
+        # fp32 gradient bucket.  NOTE: after collect(widen=False) (the FlatAdam path) its shadow
+        # slice [0, n16) is stale -- those gradients are in grad16 only; readers (grad norms,
+        # clipping, finiteness checks) must read grad16 there
         self.grad = torch.zeros(total, dtype=torch.float32, device=device)
         self.flat16 = torch.empty(self.n16, dtype=torch.bfloat16, device=device)
         self.grad16 = torch.zeros(self.n16, dtype=torch.bfloat16, device=device)
@@ -216,7 +219,35 @@ class FlatAdam:
             raise ValueError("FlatAdam: amsgrad / maximize / differentiable are not used by the reference")
         self.opt, self.fp = opt, fp
         self.p = g["params"][0]
-        self.adamw = isinstance(opt, torch.optim.AdamW)
+        if not self.p.is_cuda or self.p.dtype != torch.float32:
+            raise ValueError("FlatAdam: the flat master must be an fp32 CUDA tensor")
+        # torch >= 2.x: AdamW is Adam with decoupled_weight_decay=True, and plain Adam accepts the flag
+        self.adamw = bool(g.get("decoupled_weight_decay", isinstance(opt, torch.optim.AdamW)))
+        self._check_state()
+
+    def _check_state(self):
+        """The kernel dereferences the step counter and a tensor LR on the device: both must be
+        0-dim fp32 tensors on the master's device.  A step kept as a Python number or a host /
+        other-dtype tensor (a non-capturable optimizer, an old checkpoint) is converted here,
+        eagerly; a tensor LR elsewhere is an error (the schedule writes it in place every step)."""
+        p, g = self.p, self.opt.param_groups[0]
+        lr = g["lr"]
+        if isinstance(lr, torch.Tensor) and (lr.device != p.device or lr.dtype != torch.float32 or lr.dim() != 0):
+            raise ValueError(f"FlatAdam: a tensor lr must be a 0-dim float32 tensor on {p.device} "
+                             f"(got {lr.dtype} on {lr.device}, shape {tuple(lr.shape)})")
+        st = self.opt.state.get(p)
+        if not st:
+            return
+        step = st.get("step")
+        if step is not None and not (isinstance(step, torch.Tensor) and step.device == p.device
+                                     and step.dtype == torch.float32 and step.dim() == 0):
+            st["step"] = torch.tensor(float(step), dtype=torch.float32, device=p.device)
+        for k in ("exp_avg", "exp_avg_sq"):
+            t = st.get(k)
+            if t is None or t.device != p.device or t.dtype != torch.float32 or t.shape != p.shape \
+                    or not t.is_contiguous():
+                raise ValueError(f"FlatAdam: optimizer state {k!r} must be a contiguous fp32 tensor like the "
+                                 f"master on {p.device}")
 
     @torch.no_grad()
     def step(self, bf16_grads=True):
@@ -231,6 +262,8 @@ class FlatAdam:
             st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        elif not torch.cuda.is_current_stream_capturing():
+            self._check_state()   # a state loaded since (load_state_dict) is validated before use
         st["step"].add_(1)
         lr = g["lr"]
         lr_dev = lr if isinstance(lr, torch.Tensor) else None
