@@ -258,8 +258,8 @@ def side_stream(device, lane=0):
 class fork:
     """`with fork(device, inputs=(x, ...)) as s:` runs the block on the side
     stream after the current stream's pending work; `join(*tensors)` makes the
-    current stream wait for it and marks the tensors as used there.  No-op on
-    CPU tensors.
+    stream that is current AT THE JOIN wait for it and marks the tensors as
+    used there.  No-op on CPU tensors.
 
     Memory safety across the two streams (the caching allocator only knows the
     stream a block was allocated on):
@@ -270,16 +270,43 @@ class fork:
         kernels run; without the record the next current-stream allocation can
         take the block while a side-stream forward or backward kernel still
         reads it.
-      * the block's outputs are recorded on the current stream by `join`."""
+      * the block's outputs are recorded on the joining stream by `join`.
+
+    Nested forks and HIP-graph capture.  Under stream
+    capture the HIP runtime torch ships (7.0.51831) files every non-origin
+    stream that waits on a captured event into the waited stream's list of
+    "parallel capture streams", and at hipStreamEndCapture walks those lists
+    recursively.  A fork opened INSIDE a fork (side stream S0 forks S3, then
+    S0 waits on S3 at the join) files S3 under S0 and S0 under S3: the walk
+    never ends and the process dies of a stack overflow inside capture_end
+    (tools/capture_topology.hip reproduces it without torch; /opt/rocm 7.2's
+    runtime has no such cycle).  Hence, while capturing, a nested fork
+      * with base="outer" forks from the OUTERMOST fork's origin stream instead
+        of the current side stream -- valid when the block reads only tensors
+        that were ready there (the caller's promise) -- so the only side-to-side
+        edge is the join, and no cycle forms;
+      * otherwise runs inline on the current stream (no overlap, same result).
+    Eagerly (no capture) both run as ordinary nested forks."""
 
     # PCOPS_SIDE_STREAMS=0 runs every block on the current stream (A/B runs, and
     # the only safe way to put hipBLASLt GEMMs inside a forked block)
     enabled = os.environ.get("PCOPS_SIDE_STREAMS", "1") != "0"
 
-    def __init__(self, device, lane=0, inputs=()):
+    def __init__(self, device, lane=0, inputs=(), base="current"):
+        if base not in ("current", "outer"):
+            raise ValueError(f"fork: base must be 'current' or 'outer', not {base!r}")
         self.on = fork.enabled and torch.device(device).type == "cuda"
+        self.inline = False
         if self.on:
-            self.main = torch.cuda.current_stream(device)
+            stack = getattr(_TLS, "mains", None) or []
+            cur = torch.cuda.current_stream(device)
+            if stack and torch.cuda.is_current_stream_capturing():
+                if base == "outer":
+                    cur = stack[0]
+                else:
+                    self.on, self.inline = False, True
+                    return
+            self.main = cur
             self.side = side_stream(device, lane)
             self.inputs = tuple(t for t in inputs if isinstance(t, torch.Tensor) and t.is_cuda)
 
@@ -290,21 +317,26 @@ class fork:
                 t.record_stream(self.side)
             self._ctx = torch.cuda.stream(self.side)
             self._ctx.__enter__()
+            if not hasattr(_TLS, "mains"):
+                _TLS.mains = []
+            _TLS.mains.append(self.main)
             _TLS.side = getattr(_TLS, "side", 0) + 1
         return self
 
     def __exit__(self, *exc):
         if self.on:
             _TLS.side -= 1
+            _TLS.mains.pop()
             self._ctx.__exit__(*exc)
         return False
 
     def join(self, *tensors):
         if self.on:
-            self.main.wait_stream(self.side)
+            cur = torch.cuda.current_stream(self.side.device)
+            cur.wait_stream(self.side)
             for t in tensors:
                 if isinstance(t, torch.Tensor) and t.is_cuda:
-                    t.record_stream(self.main)
+                    t.record_stream(cur)
         return tensors[0] if len(tensors) == 1 else tensors
 
 

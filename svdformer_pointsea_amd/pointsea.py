@@ -219,9 +219,11 @@ class local_encoder(nn.Module):
 
     def forward(self, inp):
         # the FPS depends on the input cloud only: PCOPS_LOCAL_FPS_FORK=1 runs it on a stream of its
-        # own (lane 3, nested in the model's lane-0 local-encoder fork) beside gcn_1
+        # own (lane 3) beside gcn_1.  This block already runs in the model's lane-0 fork; `inp` was
+        # produced before that fork, so the inner fork may start from the outer fork's origin
+        # stream -- the form that stays capturable (_lib.fork)
         if _LOCAL_FPS_FORK:
-            with fork(inp.device, lane=3, inputs=(inp,)) as br:
+            with fork(inp.device, lane=3, inputs=(inp,), base="outer") as br:
                 idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
             x1 = self.gcn_1(inp)
             idx = br.join(idx)

@@ -8,7 +8,9 @@ replays once and compares with eager):
   fps_only    the inner block the libpcops FPS (forward only, nothing differentiable)
   full        tests/test_gpu_capture_fork.py's minimal case (forward + backward)
   flat_fps    the FPS fork opened from the ORIGIN stream (sibling of lane 0), joined into lane 0
-tools/segv_bt.so prints the native backtrace on SIGSEGV / SIGABRT.
+tools/segv_bt.so prints the native backtrace on SIGSEGV / SIGABRT.  Since the round-5 fix a nested
+fork under capture runs inline (base="current", the default here), so copy_only / fps_only / full
+no longer reach the runtime's cycle; tools/capture_topology.hip still does, torch-free.
 """
 import ctypes
 import os
@@ -33,7 +35,9 @@ def body(variant, x, w):
             f = torch.tanh(torch.einsum("oc,bcn->bon", w, x_cm))
             idx = b3.join(idx)
             g = gather_operation(f.contiguous(), idx)
-        return br.join(g).square().sum(), idx
+        g = br.join(g)
+        body.extra = (f.detach(), g.detach())
+        return g.square().sum(), idx
     with _lib.fork(x.device, inputs=(x_cm,)) as br:
         with _lib.fork(x.device, lane=3, inputs=(x_cm,)) as b3:
             if variant == "copy_only":
@@ -58,10 +62,11 @@ def main():
 
     def run():
         w.grad = None
+        body.extra = ()
         loss, idx = body(variant, x, w)
         if w.requires_grad:
             loss.backward()
-        return loss.detach(), idx
+        return (loss.detach(), idx) + body.extra
 
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -79,6 +84,20 @@ def main():
     torch.cuda.synchronize()
     ok = all(torch.equal(a, b) for a, b in zip(out, ref))
     print(f"{variant}: replay equal to eager: {ok}", flush=True)
+    for k in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        print(f"  replay {k}: loss {out[0].item()}", flush=True)
+    names = ("loss", "idx", "f", "g")
+    for name, a, b in zip(names, out, ref):
+        print(f"  {name}: equal {torch.equal(a, b)}; graph {a.flatten()[:6].tolist()} eager {b.flatten()[:6].tolist()}; "
+              f"mismatches {(a != b).sum().item()} of {a.numel()}", flush=True)
+    # a second eager run: is the eager result itself reproducible?
+    with torch.cuda.stream(side):
+        again = run()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    print(f"  eager run-to-run equal: {all(torch.equal(a, b) for a, b in zip(again, ref))}", flush=True)
     sys.exit(0 if ok else 1)
 
 

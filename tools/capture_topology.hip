@@ -48,6 +48,9 @@ static hipError_t wait_stream(hipStream_t waiter, hipStream_t waited) {
 
 int main(int argc, char **argv) {
   const char *v = argc > 1 ? argv[1] : "flat";
+  int rtv = 0;
+  CK(hipRuntimeGetVersion(&rtv));
+  printf("%s: HIP runtime %d\n", v, rtv);
   const int n = 1 << 16;
   float *a, *b, *c;
   CK(hipMalloc(&a, n * 4));
