@@ -288,6 +288,7 @@ def kernel_work(name, a):
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
             "attention bwd": "attn_(delta2|dkv3|dqs)_kernel",
             "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream|wave)_kernel",
+            "furthest_point_sampling_counts": "fps_reg_kernel<[0-9]+, (true|false), true>",
             "chamfer_3D.forward": (r"chamfer_(nn|screen|mfma|cull|cull_prep)_kernel", r"chamfer_(nn|screen|mfma|cull)_kernel"), "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
             "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",
             "colsum": ("colsum", "colsum_partial"),
@@ -391,6 +392,13 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
     fps = {}
     for e0, e1, a in spans.get("furthest_point_sampling", []):
         f = fps.setdefault(f"B{a[1]} {a[2]}->{a[3]}", [0, 0.0, a[3]])
+        f[0] += 1
+        f[1] += e0.elapsed_time(e1)
+    # the zero-padded crop clouds with per-cloud valid counts (xyz, counts, B, N, M, ...): N is
+    # the padded width; the sweep stops at each cloud's count (no algorithmic bytes credited --
+    # the counts live on the device)
+    for e0, e1, a in spans.get("furthest_point_sampling_counts", []):
+        f = fps.setdefault(f"B{a[2]} <={a[3]}->{a[4]} (counts)", [0, 0.0, a[4]])
         f[0] += 1
         f[1] += e0.elapsed_time(e1)
     out["fps_us_per_round"] = {k: round(v[1] * 1e3 / v[0] / max(1, v[2] - 1), 3) for k, v in fps.items()}
@@ -852,6 +860,13 @@ def train_leg(args, wl, batch, amp, steps, warmup, device, world, rank, use_dist
             grad_sync()
             g_opt.replay()
             schedule.batch_end()
+        # one untimed replay first: the FIRST launch of the captured PointSea step gives the
+        # MIOpen-run ResNet layers 1-3 gradients off by up to 3 % (later launches match eager within
+        # its run-to-run spread; tools/capture_grad_report.py) -- a train step like
+        # the warm-up ones, outside the clock
+        step()
+        torch.cuda.synchronize()
+        check_finite("the first graph replay")
         span_steps = args.timing_steps
     else:
         step = eager_step

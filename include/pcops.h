@@ -50,6 +50,14 @@ int pcops_abi_version(void);
 unsigned long long pcops_fps_workspace_bytes(int B, int N);
 int pcops_furthest_point_sampling(const float *xyz, int B, int N, int M, int *idx, void *workspace,
                                   unsigned long long workspace_bytes, pcops_stream_t stream);
+/* The same over zero-padded clouds whose valid rows are known: counts (B,) int32 on the device;
+ * row k >= counts[b] of cloud b is absent -- the result equals pcops_furthest_point_sampling on the
+ * buffer whose rows >= counts[b] are zero (sampling_gpu.cu:100-101 skips |p|^2 <= 1e-3 rows), and
+ * the sweep stops at the count.  Caller: seprate_point_cloud's batched crop (utils/helpers.py:
+ * 79-119 runs FPS per sample on the ragged clouds). Same workspace as above. */
+int pcops_furthest_point_sampling_counts(const float *xyz, const int *counts, int B, int N, int M, int *idx,
+                                         void *workspace, unsigned long long workspace_bytes,
+                                         pcops_stream_t stream);
 
 /* gather_points(points, idx): sampling.cpp:15-38, sampling_gpu.cu:8-30.
  * points (B,C,N), idx (B,M) -> out (B,C,M). */

@@ -29,6 +29,7 @@ _SIGS = {
     "pcops_abi_version": (I, []),
     "pcops_fps_workspace_bytes": (ULL, [I, I]),
     "pcops_furthest_point_sampling": (I, [P, I, I, I, P, P, ULL, P]),
+    "pcops_furthest_point_sampling_counts": (I, [P, P, I, I, I, P, P, ULL, P]),
     "pcops_gather_points": (I, [P, P, I, I, I, I, P, P]),
     "pcops_gather_points_grad": (I, [P, P, I, I, I, I, P, P]),
     "pcops_group_points": (I, [P, P, I, I, I, I, I, P, P]),

@@ -2121,7 +2121,7 @@ extern "C" int pcops_attention_bwd_dq_delta_colsum(const void *q, const void *k,
   if (!dq_colsum) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   if (BH == 0) return PCOPS_OK;
-  if (Lq == 0) return hipMemsetAsync(dq_colsum, 0, (size_t)H * D * sizeof(float), s) == hipSuccess ? PCOPS_OK
+  if (Lq == 0) return pc_memset_async(dq_colsum, 0, (size_t)H * D * sizeof(float), s) == hipSuccess ? PCOPS_OK
                                                                                               : PCOPS_ERR_LAUNCH;
   if (!q || !k || !v || !o || !dout || !lse || !dq || Lk <= 0) return PCOPS_ERR_INVALID;
   if (!workspace || workspace_bytes < pcops_attention_bwd_colsum_workspace_bytes(B, H, Lq, Lk, D))
@@ -2152,8 +2152,8 @@ extern "C" int pcops_attention_bwd_dkv_colsum(const void *q, const void *k, cons
   hipStream_t s = (hipStream_t)stream;
   if (BH == 0) return PCOPS_OK;
   if (Lk == 0) {
-    if (hipMemsetAsync(dk_colsum, 0, (size_t)H * D * sizeof(float), s) != hipSuccess ||
-        hipMemsetAsync(dv_colsum, 0, (size_t)H * D * sizeof(float), s) != hipSuccess)
+    if (pc_memset_async(dk_colsum, 0, (size_t)H * D * sizeof(float), s) != hipSuccess ||
+        pc_memset_async(dv_colsum, 0, (size_t)H * D * sizeof(float), s) != hipSuccess)
       return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
@@ -2238,7 +2238,7 @@ extern "C" int pcops_attention_bwd_fused(const void *q, const void *k, const voi
     }
     if (sums)
       for (float *p : {dq_colsum, dk_colsum, dv_colsum})
-        if (hipMemsetAsync(p, 0, (size_t)H * D * sizeof(float), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+        if (pc_memset_async(p, 0, (size_t)H * D * sizeof(float), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!q || !k || !v || !o || !dout || !lse || !dq || !dk || !dv || !workspace) return PCOPS_ERR_INVALID;

@@ -447,8 +447,8 @@ extern "C" int pcops_batchnorm_bwd(const void *dy, const void *y, const void *x,
   if (rows < 0 || C <= 0 || (dtype != 0 && dtype != 1) || act < 0 || act > 2) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   if (rows == 0) {
-    if ((dgamma && hipMemsetAsync(dgamma, 0, sizeof(float) * C, s) != hipSuccess) ||
-        (dbeta && hipMemsetAsync(dbeta, 0, sizeof(float) * C, s) != hipSuccess))
+    if ((dgamma && pc_memset_async(dgamma, 0, sizeof(float) * C, s) != hipSuccess) ||
+        (dbeta && pc_memset_async(dbeta, 0, sizeof(float) * C, s) != hipSuccess))
       return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }

@@ -1035,9 +1035,9 @@ int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a
   if (dsum && ((dsum_src == 1 && !dx16) || (dsum_src == 0 && !dx32) || (dsum_src != 0 && dsum_src != 1)))
     return PCOPS_ERR_INVALID;
   if (rows == 0) {
-    if (hipMemsetAsync(dgamma, 0, sizeof(float) * C, s) != hipSuccess ||
-        hipMemsetAsync(dbeta, 0, sizeof(float) * C, s) != hipSuccess ||
-        (dsum && hipMemsetAsync(dsum, 0, sizeof(float) * C, s) != hipSuccess))
+    if (pc_memset_async(dgamma, 0, sizeof(float) * C, s) != hipSuccess ||
+        pc_memset_async(dbeta, 0, sizeof(float) * C, s) != hipSuccess ||
+        (dsum && pc_memset_async(dsum, 0, sizeof(float) * C, s) != hipSuccess))
       return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
@@ -1125,7 +1125,7 @@ extern "C" int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, l
   if (C % 8) return PCOPS_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (rows == 0) {
-    if (dsum && hipMemsetAsync(dsum, 0, sizeof(float) * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    if (dsum && pc_memset_async(dsum, 0, sizeof(float) * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!dy || !u || !du) return PCOPS_ERR_INVALID;
@@ -1166,7 +1166,7 @@ extern "C" int pcops_colsum_ld(const void *g, int g_dtype, long long rows, int C
   if (C % 8 || ld % 8) return PCOPS_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (rows == 0) {
-    if (hipMemsetAsync(out, 0, (size_t)C * (out_dtype == 0 ? 4 : 2), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    if (pc_memset_async(out, 0, (size_t)C * (out_dtype == 0 ? 4 : 2), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!g) return PCOPS_ERR_INVALID;
@@ -1217,7 +1217,7 @@ extern "C" int pcops_wgrad_skinny(const void *g, const void *x, long long T, int
   if (Ci != 6 || Co % 8 || Co > 64 || (Co * Ci) % 4) return PCOPS_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (T == 0) {
-    if (hipMemsetAsync(dw, 0, (size_t)Co * Ci * (dw_dtype == 0 ? 4 : 2), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    if (pc_memset_async(dw, 0, (size_t)Co * Ci * (dw_dtype == 0 ? 4 : 2), s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!g || !x) return PCOPS_ERR_INVALID;

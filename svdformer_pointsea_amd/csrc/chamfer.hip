@@ -1069,9 +1069,9 @@ extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B
   if (!xyz1 || !xyz2 || (N && (!dist1 || !idx1)) || (M && (!dist2 || !idx2))) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   if (N == 0 || M == 0) {  // reference leaves the zero-initialised outputs untouched
-    if (N && (hipMemsetAsync(dist1, 0, sizeof(float) * B * N, s) || hipMemsetAsync(idx1, 0, sizeof(int) * B * N, s)))
+    if (N && (pc_memset_async(dist1, 0, sizeof(float) * B * N, s) || pc_memset_async(idx1, 0, sizeof(int) * B * N, s)))
       return PCOPS_ERR_LAUNCH;
-    if (M && (hipMemsetAsync(dist2, 0, sizeof(float) * B * M, s) || hipMemsetAsync(idx2, 0, sizeof(int) * B * M, s)))
+    if (M && (pc_memset_async(dist2, 0, sizeof(float) * B * M, s) || pc_memset_async(idx2, 0, sizeof(int) * B * M, s)))
       return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
@@ -1196,8 +1196,8 @@ extern "C" int pcops_chamfer_backward(const float *xyz1, const float *xyz2, int 
   if (B == 0 || (N == 0 && M == 0)) return PCOPS_OK;
   hipStream_t s = (hipStream_t)stream;
   if (N == 0 || M == 0) {
-    if (N && hipMemsetAsync(gradxyz1, 0, sizeof(float) * 3 * B * N, s)) return PCOPS_ERR_LAUNCH;
-    if (M && hipMemsetAsync(gradxyz2, 0, sizeof(float) * 3 * B * M, s)) return PCOPS_ERR_LAUNCH;
+    if (N && pc_memset_async(gradxyz1, 0, sizeof(float) * 3 * B * N, s)) return PCOPS_ERR_LAUNCH;
+    if (M && pc_memset_async(gradxyz2, 0, sizeof(float) * 3 * B * M, s)) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!xyz1 || !xyz2 || !graddist1 || !graddist2 || !idx1 || !idx2 || !gradxyz1 || !gradxyz2)

@@ -125,3 +125,43 @@ __device__ __forceinline__ void lds_barrier() {
     hipError_t _e = hipGetLastError();                  \
     if (_e != hipSuccess) return PCOPS_ERR_LAUNCH;      \
   } while (0)
+
+// ---- stream-ordered fill (replaces hipMemsetAsync everywhere in the library) ----
+// A hipMemsetAsync captured into a graph with the HIP runtime torch ships (7.0.51831) is correct
+// on the graph's FIRST launch only: later launches leave the buffer holding other values
+// (tools/capture_memset_probe.py: 1.2e9 where 0 was due, replay 2 onward), which corrupted every
+// "zero, then accumulate" output in the replayed train step.  A kernel node has
+// no such problem, so every fill in libpcops is this kernel.  `pattern` is the 32-bit word to
+// repeat (0 for zeros, 0xFFFFFFFF for the -NaN sentinel); the byte order is little-endian, so a
+// byte-granular head/tail writes the matching byte of the pattern.
+namespace {
+__global__ void pc_fill_kernel(unsigned char *__restrict__ p, size_t bytes, unsigned pattern) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  // head up to 16-B alignment, then 16-B stores, then the tail (address-based pattern phase)
+  const size_t head = (16 - ((uintptr_t)p & 15)) & 15;
+  const size_t h = head < bytes ? head : bytes;
+  if (tid < h) p[tid] = (unsigned char)(pattern >> (8 * (((uintptr_t)p + tid) & 3)));
+  const size_t body = (bytes - h) / 16;
+  uint4 *q = (uint4 *)(p + h);
+  const unsigned rot = (unsigned)(((uintptr_t)p + h) & 3);  // 0: p + h is 16-B aligned
+  const unsigned w = rot ? ((pattern >> (8 * rot)) | (pattern << (32 - 8 * rot))) : pattern;
+  const uint4 v = make_uint4(w, w, w, w);
+  for (size_t i = tid; i < body; i += stride) q[i] = v;
+  const size_t t0 = h + body * 16;
+  if (tid < bytes - t0) p[t0 + tid] = (unsigned char)(pattern >> (8 * (((uintptr_t)p + t0 + tid) & 3)));
+}
+}  // namespace
+
+// hipMemsetAsync's contract (bytes of value `byte`), as a kernel: returns hipSuccess or the launch
+// error.  Grid: one 16-B store per thread up to 2048 blocks of 256.
+static inline hipError_t pc_memset_async(void *p, int byte, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  const unsigned b = (unsigned)byte & 0xFFu;
+  const size_t vec = bytes / 16 + 32;
+  size_t blocks = (vec + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(pc_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (unsigned char *)p, bytes,
+                     b * 0x01010101u);
+  return hipGetLastError();
+}

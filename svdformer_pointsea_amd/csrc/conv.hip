@@ -523,7 +523,7 @@ extern "C" int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, 
   if (N < 0 || H < 0 || W < 0 || !dw || (dw_dtype != 0 && dw_dtype != 1)) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   if (N == 0 || H == 0 || W == 0) {
-    if (hipMemsetAsync(dw, 0, (dw_dtype == 0 ? 4 : 2) * 9 * C * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    if (pc_memset_async(dw, 0, (dw_dtype == 0 ? 4 : 2) * 9 * C * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!conv_ok(N, H, W, C)) return PCOPS_ERR_UNSUPPORTED;
@@ -568,7 +568,7 @@ extern "C" int pcops_conv3x3_c1_wgrad(const float *x, const void *dy, int N, int
   if (N < 0 || H < 0 || W < 0 || !dw || (dw_dtype != 0 && dw_dtype != 1)) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   if (N == 0 || H == 0 || W == 0) {
-    if (hipMemsetAsync(dw, 0, (dw_dtype == 0 ? 4 : 2) * kC1Out * 9, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    if (pc_memset_async(dw, 0, (dw_dtype == 0 ? 4 : 2) * kC1Out * 9, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!x || !dy) return PCOPS_ERR_INVALID;

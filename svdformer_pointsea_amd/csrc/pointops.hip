@@ -209,7 +209,7 @@ extern "C" int pcops_sa_group_grad(const void *grad_out, int grad_dtype, const i
   if (B < 0 || N < 0 || S < 0 || K < 0 || C < 0 || (grad_dtype != 0 && grad_dtype != 1)) return PCOPS_ERR_INVALID;
   if ((size_t)B * N * C == 0) return PCOPS_OK;
   if (!grad_points_t) return PCOPS_ERR_INVALID;
-  if (hipMemsetAsync(grad_points_t, 0, sizeof(float) * (size_t)B * N * C, (hipStream_t)stream) != hipSuccess)
+  if (pc_memset_async(grad_points_t, 0, sizeof(float) * (size_t)B * N * C, (hipStream_t)stream) != hipSuccess)
     return PCOPS_ERR_LAUNCH;
   const size_t total = (size_t)B * S * K * C;
   if (total == 0) return PCOPS_OK;
@@ -237,7 +237,7 @@ extern "C" int pcops_group_points_grad(const float *grad_out, const int *idx, in
   if (B < 0 || C < 0 || N < 0 || S < 0 || K < 0) return PCOPS_ERR_INVALID;
   if ((size_t)B * C * N == 0) return PCOPS_OK;
   if (!grad_points) return PCOPS_ERR_INVALID;
-  if (hipMemsetAsync(grad_points, 0, sizeof(float) * (size_t)B * C * N, (hipStream_t)stream) != hipSuccess)
+  if (pc_memset_async(grad_points, 0, sizeof(float) * (size_t)B * C * N, (hipStream_t)stream) != hipSuccess)
     return PCOPS_ERR_LAUNCH;
   const size_t total = (size_t)B * C * S * K;
   if (total == 0) return PCOPS_OK;
@@ -289,7 +289,7 @@ extern "C" int pcops_three_interpolate_grad(const float *grad_out, const int *id
   if (B < 0 || C < 0 || M < 0 || N < 0) return PCOPS_ERR_INVALID;
   if ((size_t)B * C * M == 0) return PCOPS_OK;
   if (!grad_points) return PCOPS_ERR_INVALID;
-  if (hipMemsetAsync(grad_points, 0, sizeof(float) * (size_t)B * C * M, (hipStream_t)stream) != hipSuccess)
+  if (pc_memset_async(grad_points, 0, sizeof(float) * (size_t)B * C * M, (hipStream_t)stream) != hipSuccess)
     return PCOPS_ERR_LAUNCH;
   const size_t total = (size_t)B * C * N;
   if (total == 0) return PCOPS_OK;
@@ -584,7 +584,7 @@ extern "C" int pcops_edge_group_grad(const void *grad_out, int grad_dtype, const
   if (!grad_x) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   if (K == 0) {
-    if (hipMemsetAsync(grad_x, 0, sizeof(float) * (size_t)B * N * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    if (pc_memset_async(grad_x, 0, sizeof(float) * (size_t)B * N * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!grad_out || !idx) return PCOPS_ERR_INVALID;

@@ -254,7 +254,7 @@ extern "C" int pcops_points2depth(const float *points, const float *rot, const f
   if (!workspace || workspace_bytes < pcops_points2depth_workspace_bytes(B, V, H, W)) return PCOPS_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
   float *wsum = (float *)workspace;
-  if (hipMemsetAsync(img, 0, tot * sizeof(float), s) || hipMemsetAsync(wsum, 0, tot * sizeof(float), s))
+  if (pc_memset_async(img, 0, tot * sizeof(float), s) || pc_memset_async(wsum, 0, tot * sizeof(float), s))
     return PCOPS_ERR_LAUNCH;
   const size_t np = (size_t)B * V * N;
   if (np) {
@@ -273,7 +273,7 @@ extern "C" int pcops_points2grid(const float *points, const float *rot, const fl
   if (B == 0 || V == 0) return PCOPS_OK;
   if (!points || !rot || !rot2 || !trans || !grid) return PCOPS_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(grid, 0, sizeof(float) * (size_t)B * V * D * R * R, s)) return PCOPS_ERR_LAUNCH;
+  if (pc_memset_async(grid, 0, sizeof(float) * (size_t)B * V * D * R * R, s)) return PCOPS_ERR_LAUNCH;
   hipLaunchKernelGGL(points2grid_kernel, dim3(B * V), dim3(kGridThreads), 0, s, points, rot, rot2, trans, N, V, R, D,
                      grid);
   PC_CHECK_LAUNCH();
@@ -296,7 +296,7 @@ extern "C" int pcops_grid2image(const float *grid, const float *kern, int BV, in
   const size_t RR = (size_t)R * R;
   float *raw = (float *)workspace;
   int *mx = (int *)((char *)workspace + ((BV * RR * sizeof(float) + 63) / 64) * 64);
-  if (hipMemsetAsync(mx, 0xff, sizeof(int) * BV, s)) return PCOPS_ERR_LAUNCH;  // -NaN bits < any valid max
+  if (pc_memset_async(mx, 0xff, sizeof(int) * BV, s)) return PCOPS_ERR_LAUNCH;  // -NaN bits < any valid max
   // 0xffffffff as int is -1: below every non-negative float bit pattern
   const dim3 gdim((R + kTile - 1) / kTile, (R + kTile - 1) / kTile, BV);
   hipLaunchKernelGGL(grid2image_kernel, gdim, dim3(256), 0, s, grid, kern, D, R, raw, mx);

@@ -69,9 +69,14 @@ __device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
 // Measured: ALLRED wins with 8 waves (32x2048->512: 0.318 -> 0.307 ms) and
 // loses with 16, where 16 concurrent reductions contend for the VALU
 // (32x16384->2048: 2.78 -> 2.91 ms), so 16-wave blocks keep the leader.
-template <int PPT, bool ALLRED>
+// CNT: per-cloud valid counts (pcops_furthest_point_sampling_counts) -- points k >= counts[b] are
+// absent, exactly as the reference treats the zero rows of a zero-padded buffer (|p|^2 <= 1e-3:
+// never selected, never updated); slot i of this wave covers k in [T*(PPT*half + i), +T), so the
+// slots wholly past the count are skipped by a wave-uniform branch.
+template <int PPT, bool ALLRED, bool CNT = false>
 __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
-                                                        int NWT, int SPLIT, int *__restrict__ idx) {
+                                                        int NWT, int SPLIT, int *__restrict__ idx,
+                                                        const int *__restrict__ counts = nullptr) {
   const int b = blockIdx.x;
   const float *p = xyz + (size_t)b * N * 3;
   int *out = idx + (size_t)b * M;
@@ -83,6 +88,9 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
   const bool active = rkey < T;
   const int tref = active ? (int)bitrev_bits((unsigned)rkey, L) : 0;
   const int kbase = tref + T * PPT * half;
+  const int nb = CNT ? min(max(counts[b], 0), N) : N;
+  // slots of this wave holding any point below nb (wave-uniform)
+  const int nsl = CNT ? __builtin_amdgcn_readfirstlane((nb + T - 1) / T - PPT * half) : PPT;
 
   typedef float fvec __attribute__((ext_vector_type(PPT)));
   typedef int ivec __attribute__((ext_vector_type(PPT)));
@@ -91,7 +99,7 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
 #pragma unroll
   for (int i = 0; i < PPT; ++i) {
     const int k = kbase + T * i;
-    if (active && k < N) {
+    if (active && k < nb) {
       px[i] = p[3 * k];
       py[i] = p[3 * k + 1];
       pz[i] = p[3 * k + 2];
@@ -124,14 +132,16 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
     int best = kNeverBits;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      int d = fbits(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz));
-      // PPT >= 16: keep the distance chains scalar -- LLVM's SLP pass pairs
-      // them into v_pk_add/mul/fma_f32, which on gfx950 issue at half rate
-      // and add hazard s_nops (16384->2048: 2.78 -> 2.49 ms scalar); at small
-      // PPT the packed form measured slightly faster, so it is left there
-      if constexpr (PPT >= 16) asm volatile("" : "+v"(d));
-      tmp[i] = min(d, tmp[i]);
-      best = max(best, tmp[i]);
+      if (!CNT || i < nsl) {   // slots wholly past the count hold no point (wave-uniform branch)
+        int d = fbits(sqd3(px[i] - ox, py[i] - oy, pz[i] - oz));
+        // PPT >= 16: keep the distance chains scalar -- LLVM's SLP pass pairs
+        // them into v_pk_add/mul/fma_f32, which on gfx950 issue at half rate
+        // and add hazard s_nops (16384->2048: 2.78 -> 2.49 ms scalar); at small
+        // PPT the packed form measured slightly faster, so it is left there
+        if constexpr (PPT >= 16) asm volatile("" : "+v"(d));
+        tmp[i] = min(d, tmp[i]);
+        best = max(best, tmp[i]);
+      }
     }
     FPS_STAMP(0)
     const int wmax = wave_max_i32(best);
@@ -225,9 +235,11 @@ __global__ __launch_bounds__(ALLRED ? 512 : 1024) void fps_reg_kernel(const floa
 // slots is VALU-bound where 8 waves split it), so it runs only up to 8 slots per lane (<= 512 points).
 template <int PPL>
 __global__ __launch_bounds__(64) void fps_wave_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
-                                                      int R, int PPT, int *__restrict__ idx) {
+                                                      int R, int PPT, int *__restrict__ idx,
+                                                      const int *__restrict__ counts) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const float *p = xyz + (size_t)b * N * 3;
+  const int nb = counts ? min(max(counts[b], 0), N) : N;
   int *out = idx + (size_t)b * M;
   constexpr int kNeverBits = 0xBF800000;  // -1.0f
   float px[PPL], py[PPL], pz[PPL];
@@ -237,7 +249,7 @@ __global__ __launch_bounds__(64) void fps_wave_kernel(const float *__restrict__ 
     const int j = s / PPT, i = s - j * PPT;  // PPT is uniform; s, j, i compile-time per slot only when PPT is
     const int r = lane * R + j;
     const int k = (int)bitrev_bits((unsigned)r, L) + T * i;
-    if (j < R && r < T && k < N) {
+    if (j < R && r < T && k < nb) {
       px[s] = p[3 * k];
       py[s] = p[3 * k + 1];
       pz[s] = p[3 * k + 2];
@@ -296,15 +308,17 @@ struct __align__(16) FpsSlot {
 // (L2-resident after the first round) and running distances in the workspace.
 __global__ __launch_bounds__(kFpsThreads) void fps_stream_kernel(const float *__restrict__ xyz, int N, int M, int T,
                                                                   int L, float *__restrict__ temp,
-                                                                  int *__restrict__ idx) {
+                                                                  int *__restrict__ idx,
+                                                                  const int *__restrict__ counts) {
   const int b = blockIdx.x;
+  const int nb = counts ? min(max(counts[b], 0), N) : N;
   const float *p = xyz + (size_t)b * N * 3;
   float *tm = temp + (size_t)b * N;
   int *out = idx + (size_t)b * M;
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int nw = blockDim.x >> 6;
-  for (int k = t; k < N; k += blockDim.x) {
+  for (int k = t; k < nb; k += blockDim.x) {
     const float mag = sqd3(p[3 * k], p[3 * k + 1], p[3 * k + 2]);
     tm[k] = ((double)mag <= 1e-3) ? -1.f : 1e10f;
   }
@@ -318,7 +332,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_stream_kernel(const float *__
     float best = -1.f;
     int bk = 0;
     if (t < T) {
-      for (int k = t; k < N; k += T) {
+      for (int k = t; k < nb; k += T) {
         const float d = sqd3(p[3 * k] - ox, p[3 * k + 1] - oy, p[3 * k + 2] - oz);
         const float d2 = fminf(d, tm[k]);
         tm[k] = d2;
@@ -452,8 +466,9 @@ extern "C" unsigned long long pcops_fps_workspace_bytes(int B, int N) {
   return (N > kFpsThreads * kFpsMaxPPT) ? (unsigned long long)B * N * sizeof(float) : 0ull;
 }
 
-extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int M, int *idx, void *workspace,
-                                             unsigned long long workspace_bytes, pcops_stream_t stream) {
+namespace {
+int fps_impl(const float *xyz, const int *counts, int B, int N, int M, int *idx, void *workspace,
+             unsigned long long workspace_bytes, pcops_stream_t stream) {
   if (B < 0 || M < 0 || (M > 0 && N <= 0)) return PCOPS_ERR_INVALID;
   if (B == 0 || M == 0) return PCOPS_OK;
   if (!xyz || !idx) return PCOPS_ERR_INVALID;
@@ -473,7 +488,7 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
     const int ppl = R * ppt;
 #define FPS_WAVE_CASE(P)                                                                                     \
   if (ppl <= P) {                                                                                            \
-    hipLaunchKernelGGL((fps_wave_kernel<P>), dim3(B), dim3(64), 0, s, xyz, N, M, T, L, R, ppt, idx);        \
+    hipLaunchKernelGGL((fps_wave_kernel<P>), dim3(B), dim3(64), 0, s, xyz, N, M, T, L, R, ppt, idx, counts); \
     PC_CHECK_LAUNCH();                                                                                       \
     return PCOPS_OK;                                                                                         \
   }
@@ -492,29 +507,51 @@ extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int
     const int split = (ppt > fps_split_ppt() && T == 512) ? 2 : 1;
     const int per = (ppt + split - 1) / split;
     const int nwt = nthreads / 64;
+#define FPS_LAUNCH(P, AR, CN)                                                                             \
+  hipLaunchKernelGGL((fps_reg_kernel<P, AR, CN>), dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt, \
+                     split, idx, counts)
 #define FPS_CASE(P)                                                                                       \
   if (per <= P) {                                                                                         \
-    if (fps_v1() || nthreads * split > 512)                                                               \
-      hipLaunchKernelGGL((fps_reg_kernel<P, false>), dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt, \
-                         split, idx);                                                                     \
-    else                                                                                                  \
-      hipLaunchKernelGGL((fps_reg_kernel<P, true>), dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt,  \
-                         split, idx);                                                                     \
+    const bool ar = !(fps_v1() || nthreads * split > 512);                                                \
+    if (counts) {                                                                                         \
+      if (ar) FPS_LAUNCH(P, true, true); else FPS_LAUNCH(P, false, true);                                 \
+    } else {                                                                                              \
+      if (ar) FPS_LAUNCH(P, true, false); else FPS_LAUNCH(P, false, false);                               \
+    }                                                                                                     \
     PC_CHECK_LAUNCH();                                                                                    \
     return PCOPS_OK;                                                                                      \
   }
+    // exact slot counts for the model's clouds (2304 -> 5 per thread, 6144 -> 12): the
+    // sweep runs every slot of the template, so a power-of-two P wasted up to 3 / 4 of 8 / 16
     FPS_CASE(1)
     FPS_CASE(2)
     FPS_CASE(4)
+    FPS_CASE(6)
     FPS_CASE(8)
+    FPS_CASE(12)
     FPS_CASE(16)
     FPS_CASE(32)
 #undef FPS_CASE
+#undef FPS_LAUNCH
   }
   if (!workspace || workspace_bytes < pcops_fps_workspace_bytes(B, N)) return PCOPS_ERR_WORKSPACE;
-  hipLaunchKernelGGL(fps_stream_kernel, dim3(B), dim3(nthreads), 0, s, xyz, N, M, T, L, (float *)workspace, idx);
+  hipLaunchKernelGGL(fps_stream_kernel, dim3(B), dim3(nthreads), 0, s, xyz, N, M, T, L, (float *)workspace, idx,
+                     counts);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
+}
+}  // namespace
+
+extern "C" int pcops_furthest_point_sampling(const float *xyz, int B, int N, int M, int *idx, void *workspace,
+                                             unsigned long long workspace_bytes, pcops_stream_t stream) {
+  return fps_impl(xyz, nullptr, B, N, M, idx, workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcops_furthest_point_sampling_counts(const float *xyz, const int *counts, int B, int N, int M, int *idx,
+                                                    void *workspace, unsigned long long workspace_bytes,
+                                                    pcops_stream_t stream) {
+  if (!counts && B > 0 && M > 0) return PCOPS_ERR_INVALID;
+  return fps_impl(xyz, counts, B, N, M, idx, workspace, workspace_bytes, stream);
 }
 
 extern "C" int pcops_gather_points(const float *points, const int *idx, int B, int C, int N, int M, float *out,
@@ -534,7 +571,7 @@ extern "C" int pcops_gather_points_grad(const float *grad_out, const int *idx, i
   if (B < 0 || C < 0 || N < 0 || M < 0) return PCOPS_ERR_INVALID;
   if ((size_t)B * C * N == 0) return PCOPS_OK;
   if (!grad_points) return PCOPS_ERR_INVALID;
-  if (hipMemsetAsync(grad_points, 0, sizeof(float) * (size_t)B * C * N, (hipStream_t)stream) != hipSuccess)
+  if (pc_memset_async(grad_points, 0, sizeof(float) * (size_t)B * C * N, (hipStream_t)stream) != hipSuccess)
     return PCOPS_ERR_LAUNCH;
   const size_t total = (size_t)B * C * M;
   if (total == 0) return PCOPS_OK;

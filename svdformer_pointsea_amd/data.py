@@ -15,13 +15,17 @@ distances (sampling_gpu.cu:100-101), the surviving points keep their
 indices, and the block size (hence the tie rule) is 512 for every N >= 512,
 so the selected indices are those of the per-sample ragged call.
 """
+import os
 import random
 
 import torch
 import torch.nn.functional as F
 
 from ._lib import fork
-from .model_utils import fps_subsample
+from .model_utils import fps_subsample, fps_subsample_counts
+
+# PCOPS_FPS_COUNTS=0: the crop FPS sweeps the whole zero-padded width (A/B runs)
+_FPS_COUNTS = os.environ.get("PCOPS_FPS_COUNTS", "1") != "0"
 
 
 def _pack(points, order, start, count, n_max):
@@ -80,14 +84,21 @@ def seprate_point_cloud(xyz, num_points, crop, fixed_points=None, padding_zeros=
         hi = int(crop[1])
         if not padding_zeros:
             input_data = _pack(xyz, order, num_crop, n - num_crop, n - int(crop[0]))
+        # the packed clouds are zero-padded past their valid rows; on the GPU the FPS sweep stops
+        # at each cloud's count (the same points: the reference skips the zero rows)
+        def fps(cloud, count):
+            if padding_zeros or not cloud.is_cuda or not _FPS_COUNTS:
+                return fps_subsample(cloud.contiguous(), 2048)
+            return fps_subsample_counts(cloud.contiguous(), count.to(torch.int32), 2048)
+
         if not want_crop:
-            return fps_subsample(input_data.contiguous(), 2048), None
+            return fps(input_data, n - num_crop), None
         crop_data = _pack(xyz, order, torch.zeros_like(num_crop), num_crop, hi)
         # the two FPS launches (B workgroups each) run side by side
         crop_data = crop_data.contiguous()
-        with fork(dev, inputs=(crop_data,)) as br:
-            crop_out = fps_subsample(crop_data, 2048)
-        input_out = fps_subsample(input_data.contiguous(), 2048)
+        with fork(dev, inputs=(crop_data, num_crop)) as br:
+            crop_out = fps(crop_data, num_crop)
+        input_out = fps(input_data, n - num_crop)
         return input_out, br.join(crop_out)
     k = int(crop)
     if not padding_zeros:

@@ -21,7 +21,7 @@ import torch
 from torch import nn
 
 from ._lib import Workspace, call, lib, ptr, require_float, stream_of
-from .pointnet2_utils import furthest_point_sample, gather_operation, grouping_operation
+from .pointnet2_utils import furthest_point_sample, furthest_point_sample_counts, gather_operation, grouping_operation
 
 
 def _knn(q, p, k, pad=0, want_dist=False):
@@ -88,6 +88,15 @@ def group_local(xyz, k=20, return_idx=False):
 def fps_subsample(pcd, n_points=2048):
     """pcd (B,N,3) -> (B,n_points,3) (model_utils.py:489-499)."""
     new_pcd = gather_operation(pcd.permute(0, 2, 1).contiguous(), furthest_point_sample(pcd.contiguous(), n_points))
+    return new_pcd.permute(0, 2, 1).contiguous()
+
+
+def fps_subsample_counts(pcd, counts, n_points=2048):
+    """fps_subsample of zero-padded clouds whose valid rows are counts (B,) int32: the FPS sweep
+    stops at each cloud's count (pointnet2_utils.furthest_point_sample_counts); the same points
+    as fps_subsample of the padded buffer."""
+    idx = furthest_point_sample_counts(pcd.contiguous(), counts, n_points)
+    new_pcd = gather_operation(pcd.permute(0, 2, 1).contiguous(), idx)
     return new_pcd.permute(0, 2, 1).contiguous()
 
 

@@ -44,6 +44,27 @@ class FurthestPointSampling(Function):
 furthest_point_sample = FurthestPointSampling.apply
 
 
+def furthest_point_sample_counts(xyz, counts, npoint):
+    """FPS over zero-padded clouds with known valid row counts (B,) int32: row k >= counts[b]
+    of cloud b is absent.  Equals furthest_point_sample on the buffer whose rows >= counts[b]
+    are zero (the reference skips |p|^2 <= 1e-3 rows, sampling_gpu.cu:100-101) -- the ragged
+    per-sample FPS calls of utils/helpers.py:79-119 -- with the sweep stopping at the count.
+    Not differentiable (as furthest_point_sample)."""
+    require_float(xyz, "points")
+    require_int(counts, "counts")
+    B, N, _ = xyz.shape
+    if counts.shape != (B,):
+        raise RuntimeError(f"counts must have shape ({B},), got {tuple(counts.shape)}")
+    npoint = int(npoint)
+    out = torch.empty(B, npoint, dtype=torch.int32, device=xyz.device)
+    wsb = lib().pcops_fps_workspace_bytes(B, N)
+    ws = _lib.Workspace.get(xyz.device, wsb)
+    with torch.cuda.device(xyz.device):
+        call("furthest_point_sampling_counts", lib().pcops_furthest_point_sampling_counts, ptr(xyz), ptr(counts), B, N,
+             npoint, ptr(out), ptr(ws), wsb, stream_of(xyz))
+    return out
+
+
 class GatherOperation(Function):
     @staticmethod
     @custom_fwd(device_type="cuda", cast_inputs=torch.float32)

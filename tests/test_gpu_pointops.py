@@ -140,6 +140,37 @@ def test_fps_full_size_properties(dev):
     np.testing.assert_array_equal(idx.cpu().numpy(), O.furthest_point_sample(x.cpu().numpy(), 2048))
 
 
+@pytest.mark.parametrize("B,N,M,tail", [(16, 6144, 2048, "zero"), (5, 6144, 2048, "garbage"),
+                                        (3, 2304, 1024, "garbage"), (2, 16384, 2048, "garbage"),
+                                        (2, 20000, 300, "garbage"), (3, 400, 100, "garbage"),
+                                        (4, 6144, 512, "edge")])
+def test_fps_counts_bitexact(dev, B, N, M, tail):
+    """pcops_furthest_point_sampling_counts (the batched crop's zero-padded clouds with known valid
+    counts): equal to the plain FPS -- and to the oracle -- on the buffer whose rows >= count are
+    zero, whatever the rows past the count hold ("garbage": they must be ignored); counts across
+    slot boundaries, counts 0 and N, and counts below the block size ("edge")."""
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample, furthest_point_sample_counts
+
+    rng = np.random.default_rng(B * N + M)
+    x = (rng.random((B, N, 3)) - 0.5).astype(np.float32)
+    if tail == "edge":
+        counts = np.array([0, N, 1, 300][:B], np.int32)
+    else:
+        counts = rng.integers(max(1, N // 3), N + 1, B).astype(np.int32)
+        counts[0] = N
+        if B > 2:
+            counts[1] = (N // 512) * 512 if N >= 512 else N // 2   # an exact slot boundary
+    z = x.copy()
+    for b in range(B):
+        z[b, counts[b]:] = 0.0
+    if tail == "zero":
+        x = z.copy()
+    got = furthest_point_sample_counts(T(x, dev), T(counts, dev), M).cpu().numpy()
+    ref = furthest_point_sample(T(z, dev), M).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(got, O.furthest_point_sample(z, M))
+
+
 # ------------------------------------------------------------------ gather / group
 def test_gather_and_grad(dev):
     from svdformer_pointsea_amd.pointnet2_utils import gather_operation
