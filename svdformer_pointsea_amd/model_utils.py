@@ -131,14 +131,42 @@ class _SAGroup(torch.autograd.Function):
         return None, None, gp, None, None
 
 
-def sample_and_group_knn_cl(xyz, points_t, npoint, k, out_dtype=torch.float32):
+class SharedFPS:
+    """Furthest-point indices of one cloud computed once for two consumers.
+
+    FPS is greedy: the first m indices of an FPS of M >= m points ARE the FPS of m points of the
+    same cloud (every round depends only on the rounds before it; the tie rule, sampling_gpu.cu:
+    69-173, depends on N, not on M).  The models sample the partial input twice -- the local
+    encoder (SVDFormer.py:177, PointSea.py:241, local_points) and the point encoder's first SA
+    module (model_utils.py:341, 512) -- so the FPS runs once, for the larger count, on the stream
+    that produced it; `take(m)` hands the first m columns to another stream after an event wait
+    (graph-capturable: the origin stream waits on a side stream's event)."""
+
+    def __init__(self, idx):
+        self.idx = idx
+        self.event = None
+        if idx.is_cuda:
+            self.event = torch.cuda.Event()
+            self.event.record(torch.cuda.current_stream(idx.device))
+
+    def take(self, m):
+        if m > self.idx.shape[1]:
+            raise ValueError(f"SharedFPS holds {self.idx.shape[1]} indices, {m} requested")
+        if self.event is not None:
+            cur = torch.cuda.current_stream(self.idx.device)
+            cur.wait_event(self.event)
+            self.idx.record_stream(cur)
+        return self.idx if m == self.idx.shape[1] else self.idx[:, :m].contiguous()
+
+
+def sample_and_group_knn_cl(xyz, points_t, npoint, k, out_dtype=torch.float32, fidx=None):
     """sample_and_group_knn (model_utils.py:323-356, use_xyz) in three launches --
     FPS, kNN, and ONE fused grouping (pcops_sa_group) that writes the
     neighbourhood features straight into the channels_last memory the first
     1x1 conv reads.  xyz (B,3,N) without gradient, points_t (B,N,C) token-major
     (or None) -> new_xyz (B,3,S), features (B,3+C,S,K) channels_last, idx."""
     xyz_t = xyz.transpose(1, 2).contiguous()
-    fidx = furthest_point_sample(xyz_t, npoint)
+    fidx = furthest_point_sample(xyz_t, npoint) if fidx is None else fidx.take(npoint)
     new_xyz = gather_operation(xyz.contiguous(), fidx)                 # (B,3,S), the reference's new_xyz
     new_xyz_t = new_xyz.transpose(1, 2).contiguous()
     idx = query_knn(k, xyz_t, new_xyz_t)
@@ -148,10 +176,10 @@ def sample_and_group_knn_cl(xyz, points_t, npoint, k, out_dtype=torch.float32):
     return new_xyz, feat.permute(0, 3, 1, 2), idx
 
 
-def sample_and_group_knn(xyz, points, npoint, k, use_xyz=True, idx=None):
+def sample_and_group_knn(xyz, points, npoint, k, use_xyz=True, idx=None, fidx=None):
     """model_utils.py:323-356: FPS -> gather -> kNN -> group (xyz, points)."""
     xyz_flipped = xyz.permute(0, 2, 1).contiguous()
-    new_xyz = gather_operation(xyz, furthest_point_sample(xyz_flipped, npoint))
+    new_xyz = gather_operation(xyz, furthest_point_sample(xyz_flipped, npoint) if fidx is None else fidx.take(npoint))
     if idx is None:
         idx = query_knn(k, xyz_flipped, new_xyz.permute(0, 2, 1).contiguous())
     grouped_xyz = grouping_operation(xyz, idx)

@@ -35,7 +35,8 @@ from .chamfer3D import chamfer_3DDist
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act
 from .pointnet2_utils import furthest_point_sample, gather_operation
-from .svdformer import MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin
+from .svdformer import (MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin,
+                        shared_partial_fps)
 
 _LOCAL_FPS_FORK = os.environ.get("PCOPS_LOCAL_FPS_FORK", "0") == "1"
 
@@ -185,11 +186,11 @@ class SVFNet(nn.Module):
         self.register_buffer("view_point", torch.tensor([0, 0, -d, -d, 0, 0, 0, d, 0], dtype=torch.float32)
                              .view(-1, 3, 3).permute(0, 2, 1).contiguous(), persistent=False)
 
-    def forward(self, points, depth):
+    def forward(self, points, depth, fidx=None):
         B, _, N = points.size()
         f_v = self.img_feature_extractor(depth.contiguous(memory_format=torch.channels_last))
         f_v = f_v.flatten(2)                                           # 'bv c h w -> bv c (h w)'
-        f_p = self.point_feature_extractor(points)                     # (B, 256, 1)
+        f_p = self.point_feature_extractor(points, fidx=fidx)          # (B, 256, 1)
         view_feature_1 = self.posmlp(self.view_point.expand(B, 3, 3))  # (B, 256, 3)
         # f_p.repeat(3, 1, n): image r (= 3b + v) is paired with f_p[r % B], as in the reference
         f_v_ = self.viewattn1(torch.cat([f_v, f_p.repeat(3, 1, f_v.size(2)).to(f_v.dtype)], 1))
@@ -217,7 +218,14 @@ class local_encoder(nn.Module):
         self.gcn_3 = EdgeConv(256, 512, 4)
         self.local_number = cfg.NETWORK.local_points
 
-    def forward(self, inp):
+    def forward(self, inp, fidx=None):
+        """fidx: a model_utils.SharedFPS of inp (the model's shared partial-cloud FPS)."""
+        if fidx is not None:
+            x1 = self.gcn_1(inp)
+            x1 = gather_operation(x1.float().contiguous(), fidx.take(self.local_number))
+            x2 = self.gcn_2(x1)
+            x3 = self.gcn_3(x2)
+            return torch.cat([x1, x2.to(x1.dtype), x3.to(x1.dtype)], 1)
         # the FPS depends on the input cloud only: PCOPS_LOCAL_FPS_FORK=1 runs it on a stream of its
         # own (lane 3) beside gcn_1.  This block already runs in the model's lane-0 fork; `inp` was
         # produced before that fork, so the inner fork may start from the outer fork's origin
@@ -255,9 +263,13 @@ class Model(nn.Module):
         # the local encoder (EdgeConv kNN, FPS, 1x1-conv GEMMs on rocBLAS: no stream-K)
         # only depends on the partial cloud: it runs on a second HIP stream
         # beside the view/point encoder
-        with fork(partial.device, inputs=(partial_cm,)) as br:
-            local_feat = self.localencoder(partial_cm)
-        feat_g, coarse = self.encoder(partial_cm, depth)
+        with fork(partial.device, inputs=(partial_cm, partial)) as br:
+            # the partial cloud's FPS once, first on this stream: the local encoder's 1024 and the
+            # point encoder's SA module's first 512 (svdformer.shared_partial_fps)
+            fidx = shared_partial_fps(partial, self.localencoder.local_number,
+                                      self.encoder.point_feature_extractor.sa_module_1.npoint)
+            local_feat = self.localencoder(partial_cm, fidx=fidx)
+        feat_g, coarse = self.encoder(partial_cm, depth, fidx=fidx)
         local_feat = br.join(local_feat)
         coarse_merge = torch.cat([partial_cm, coarse.to(partial_cm.dtype)], dim=2).float().contiguous()
         coarse_merge = gather_operation(coarse_merge, furthest_point_sample(coarse_merge.transpose(1, 2).contiguous(),

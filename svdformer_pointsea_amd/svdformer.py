@@ -22,7 +22,8 @@ from torch import nn
 from .attention import (PosEmbedding, SDG_Decoder, block_sum, cross_attention, linear, self_attention, to_channels,
                         to_tokens)
 from .chamfer3D import chamfer_3DDist
-from .model_utils import edge_features, fps_subsample, group_local, sample_and_group_knn, sample_and_group_knn_cl
+from .model_utils import (SharedFPS, edge_features, fps_subsample, group_local, sample_and_group_knn,
+                          sample_and_group_knn_cl)
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act, run_sequential
 from .conv import conv3x3
@@ -90,6 +91,9 @@ import os as _os
 
 # PCOPS_SA_FUSED=0: the unfused sample_and_group_knn path (A/B runs, parity tests)
 _SA_FUSED = _os.environ.get("PCOPS_SA_FUSED", "1") != "0"
+# PCOPS_FPS_SHARE=0: the local encoder and the first SA module each run their own FPS of the
+# partial cloud (A/B runs; the shared form gives the same indices, see model_utils.SharedFPS)
+_FPS_SHARE = _os.environ.get("PCOPS_FPS_SHARE", "1") != "0"
 _MAXK = _os.environ.get("PCOPS_MAXK", "1") != "0"   # A/B switch: pcops_max_k for the neighbourhood max
 # PCOPS_EDGE_FUSED=0: EdgeConv's unfused group_local -> repeat -> subtract -> cat path (A/B, parity tests)
 _EDGE_FUSED = _os.environ.get("PCOPS_EDGE_FUSED", "1") != "0"
@@ -277,7 +281,8 @@ class PointNet_SA_Module_KNN(nn.Module):
         self.mlp_conv = nn.Sequential(*convs)
         self.pcsa = PCSA(mlp[-1], nsample) if (not group_all and use_pcsa) else None
 
-    def forward(self, xyz, points, idx=None):
+    def forward(self, xyz, points, idx=None, fidx=None):
+        """fidx: a model_utils.SharedFPS of this xyz (its first npoint indices are this module's FPS)."""
         fused = (_SA_FUSED and not self.group_all and self.use_xyz and idx is None and xyz.is_cuda
                  and not xyz.requires_grad and points is not None)
         if fused:
@@ -286,12 +291,12 @@ class PointNet_SA_Module_KNN(nn.Module):
             # they come from the previous SA module (its output is a (B,S,C) view)
             dt = torch.bfloat16 if torch.is_autocast_enabled("cuda") else torch.float32
             new_xyz, new_points, idx = sample_and_group_knn_cl(xyz, points.transpose(1, 2), self.npoint,
-                                                               self.nsample, dt)
+                                                               self.nsample, dt, fidx=fidx)
         elif self.group_all:
             new_xyz, new_points, idx, _ = sample_and_group_all(xyz, points, self.use_xyz)
         else:
             new_xyz, new_points, idx, _ = sample_and_group_knn(xyz, points, self.npoint, self.nsample, self.use_xyz,
-                                                               idx=idx)
+                                                               idx=idx, fidx=fidx)
         new_points = self.mlp_conv(new_points.contiguous(memory_format=torch.channels_last))
         if self.pcsa is not None:
             new_points = self.pcsa(new_points)
@@ -424,8 +429,9 @@ class FeatureExtractor(nn.Module):
         self.sa_module_3 = PointNet_SA_Module_KNN(None, None, 256, [512, out_dim], group_all=True, if_bn=False,
                                                   use_pcsa=False)
 
-    def forward(self, point_cloud):
-        l1_xyz, l1_points, _ = self.sa_module_1(point_cloud, point_cloud)
+    def forward(self, point_cloud, fidx=None):
+        """fidx: a model_utils.SharedFPS of point_cloud (the model's shared partial-cloud FPS)."""
+        l1_xyz, l1_points, _ = self.sa_module_1(point_cloud, point_cloud, fidx=fidx)
         l2_xyz, l2_points, _ = self.sa_module_2(l1_xyz, l1_points)
         _, l3_points = self.sa_module_3(l2_xyz, l2_points)
         return l3_points
@@ -566,7 +572,7 @@ class SVFNet(nn.Module):
         self.register_buffer("view_point", torch.tensor([0, 0, -d, -d, 0, 0, 0, d, 0], dtype=torch.float32)
                              .view(-1, 3, 3).permute(0, 2, 1).contiguous(), persistent=False)
 
-    def forward(self, points, depth):
+    def forward(self, points, depth, fidx=None):
         batch_size, _, N = points.size()
         depth = depth.contiguous(memory_format=torch.channels_last)
         # the image branch (convs + BatchNorm, no GEMM) and the point branch (FPS, kNN, grouping,
@@ -577,7 +583,7 @@ class SVFNet(nn.Module):
             # stem conv (1 -> 16) on libpcops under bf16 autocast, each BN + ReLU fused
             f_v = run_sequential(self.img_feature_extractor, depth, conv3x3).view(batch_size, 3, -1).transpose(1, 2)
             f_v = f_v.contiguous()
-        f_p = self.point_feature_extractor(points)
+        f_p = self.point_feature_extractor(points, fidx=fidx)
         f_v = br.join(f_v)
         view_point = self.view_point.expand(batch_size, 3, 3)
         view_feature = self.posmlp(view_point).permute(2, 0, 1)
@@ -600,11 +606,24 @@ class local_encoder(nn.Module):
         self.gcn_2 = EdgeConv(64, 256, 8)
         self.local_number = cfg.NETWORK.local_points
 
-    def forward(self, inp):
+    def forward(self, inp, fidx=None):
+        """fidx: a model_utils.SharedFPS of inp (the model's shared partial-cloud FPS)."""
         x1 = self.gcn_1(inp)
-        idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
+        if fidx is None:
+            idx = furthest_point_sample(inp.transpose(1, 2).float().contiguous(), self.local_number)
+        else:
+            idx = fidx.take(self.local_number)
         x1 = gather_operation(x1.float().contiguous(), idx)
         return self.gcn_2(x1)
+
+
+def shared_partial_fps(partial, n_local, n_sa):
+    """The partial cloud's FPS for both of its consumers (model_utils.SharedFPS), computed on the
+    current stream; None when sharing is off (PCOPS_FPS_SHARE=0, A/B runs) or it would not be a
+    prefix (n_sa > n_local)."""
+    if not _FPS_SHARE or n_sa > n_local:
+        return None
+    return SharedFPS(furthest_point_sample(partial.float().contiguous(), n_local))
 
 
 class Model(nn.Module):
@@ -630,9 +649,14 @@ class Model(nn.Module):
         # the local encoder (EdgeConv kNN, FPS, 1x1-conv GEMMs on rocBLAS: no stream-K)
         # only depends on the partial cloud: it runs on a second HIP stream
         # beside the view/point encoder
-        with fork(partial.device, inputs=(partial_cm,)) as br:
-            local_feat = self.localencoder(partial_cm)
-        feat_g, coarse = self.encoder(partial_cm, depth)
+        with fork(partial.device, inputs=(partial_cm, partial)) as br:
+            # the partial cloud's FPS, once, first on this stream: the local encoder's and (the
+            # first 512 indices) the point encoder's SA module's -- the main stream takes them
+            # after the image branch, by an event wait
+            fidx = shared_partial_fps(partial, self.localencoder.local_number,
+                                      self.encoder.point_feature_extractor.sa_module_1.npoint)
+            local_feat = self.localencoder(partial_cm, fidx=fidx)
+        feat_g, coarse = self.encoder(partial_cm, depth, fidx=fidx)
         local_feat = br.join(local_feat)
         coarse_merge = torch.cat([partial_cm, coarse.to(partial_cm.dtype)], dim=2).float().contiguous()
         coarse_merge = gather_operation(coarse_merge, furthest_point_sample(coarse_merge.transpose(1, 2).contiguous(),

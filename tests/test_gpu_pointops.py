@@ -171,6 +171,27 @@ def test_fps_counts_bitexact(dev, B, N, M, tail):
     np.testing.assert_array_equal(got, O.furthest_point_sample(z, M))
 
 
+@pytest.mark.parametrize("B,N,M,m", [(4, 2048, 1024, 512), (32, 2048, 512, 512), (3, 2048, 1024, 256),
+                                     (2, 16384, 2048, 256)])
+def test_fps_prefix_property(dev, B, N, M, m):
+    """The models' shared partial-cloud FPS (model_utils.SharedFPS) rests on FPS being greedy: the
+    first m indices of an M-point FPS are the m-point FPS of the same cloud.  Bitwise, on plain and
+    on tiled (PCN-style duplicate, tie-heavy) clouds, and through SharedFPS.take on a side stream."""
+    from svdformer_pointsea_amd import _lib
+    from svdformer_pointsea_amd.model_utils import SharedFPS
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
+
+    rng = np.random.default_rng(B + N + M + m)
+    for x in ((rng.random((B, N, 3)) - 0.5).astype(np.float32), _tiled(rng, B, N // 3, N)):
+        xt = T(x, dev)
+        full = furthest_point_sample(xt, M)
+        np.testing.assert_array_equal(full[:, :m].cpu().numpy(), furthest_point_sample(xt, m).cpu().numpy())
+        with _lib.fork(dev, inputs=(xt,)):
+            sh = SharedFPS(furthest_point_sample(xt, M))
+        got = sh.take(m)
+        np.testing.assert_array_equal(got.cpu().numpy(), full[:, :m].cpu().numpy())
+
+
 # ------------------------------------------------------------------ gather / group
 def test_gather_and_grad(dev):
     from svdformer_pointsea_amd.pointnet2_utils import gather_operation

@@ -215,3 +215,13 @@ def test_ball_query_and_three_nn_oracle_semantics():
     dist, i3, d2 = O.three_nn(new, xyz)
     full = ((new[0, :, None] - xyz[0, None]) ** 2).sum(-1)
     np.testing.assert_array_equal(i3[0], np.argsort(full, -1, kind="stable")[:, :3])
+
+
+def test_fps_prefix_property_oracle():
+    """FPS is greedy: the first m indices of an M-point FPS are the m-point FPS of the same cloud
+    (the basis of the models' shared partial-cloud FPS, model_utils.SharedFPS)."""
+    rng = np.random.default_rng(7)
+    x = (rng.random((3, 2048, 3)) - 0.5).astype(np.float32)
+    x[1, 1024:] = x[1, :1024]   # exact duplicates: ties decided by the tie rule alone
+    full = O.furthest_point_sample(x, 1024)
+    np.testing.assert_array_equal(full[:, :512], O.furthest_point_sample(x, 512))

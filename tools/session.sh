@@ -1,12 +1,12 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r5t; mkdir -p $O
+O=gpurun_out/r5u; mkdir -p $O
 export TMPDIR=/tmp
-
-timeout -k 10 600 python -u -m pytest tests/test_gpu_capture_fork.py tests/test_gpu_pointops.py tests/test_gpu_pointsea.py -x -v --timeout 300 --timeout-method thread -k "capture or fps or seprate or pointsea or culled or replays" > $O/tests.log 2>&1 || exit 1
-B="--model pointsea --no-cpu-baseline --no-fp32-leg --no-extra-legs"
-for f in 1 0; do
-  PCOPS_FPS_COUNTS=$f timeout -k 10 400 python bench.py $B > $O/ps_counts$f.json 2>> $O/ps_counts$f.err || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_capture_fork.py tests/test_gpu_pointops.py tests/test_gpu_pointsea.py tests/test_gpu_model.py tests/test_gpu_sa_fused.py -x -v --timeout 300 --timeout-method thread -k "capture or fps or seprate or pointsea or replays or model or sa" > $O/tests.log 2>&1 || exit 1
+for f in 1 0 1 0; do
+  PCOPS_FPS_SHARE=$f timeout -k 10 400 python bench.py --no-cpu-baseline --no-fp32-leg --no-extra-legs > $O/pcn_share$f.json.$RANDOM 2>> $O/pcn_share$f.err || exit 1
 done
-timeout -k 10 400 python bench.py --no-cpu-baseline --no-fp32-leg --no-extra-legs > $O/pcn.json 2> $O/pcn.err || exit 1
+for f in 1 0; do
+  PCOPS_FPS_SHARE=$f timeout -k 10 400 python bench.py --model pointsea --no-cpu-baseline --no-fp32-leg --no-extra-legs > $O/ps_share$f.json 2>> $O/ps_share$f.err || exit 1
+done
