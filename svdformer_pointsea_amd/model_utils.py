@@ -144,18 +144,23 @@ class SharedFPS:
 
     def __init__(self, idx):
         self.idx = idx
-        self.event = None
+        self.event = self.stream = None
         if idx.is_cuda:
+            self.stream = torch.cuda.current_stream(idx.device)
             self.event = torch.cuda.Event()
-            self.event.record(torch.cuda.current_stream(idx.device))
+            self.event.record(self.stream)
 
     def take(self, m):
         if m > self.idx.shape[1]:
             raise ValueError(f"SharedFPS holds {self.idx.shape[1]} indices, {m} requested")
         if self.event is not None:
             cur = torch.cuda.current_stream(self.idx.device)
-            cur.wait_event(self.event)
-            self.idx.record_stream(cur)
+            # never on the producing stream itself: stream order suffices there, and under graph
+            # capture a side stream waiting on its own event files itself in its own list of
+            # parallel capture streams (HIP 7.0) -- the end-of-capture walk never returns (_lib.fork)
+            if cur != self.stream:
+                cur.wait_event(self.event)
+                self.idx.record_stream(cur)
         return self.idx if m == self.idx.shape[1] else self.idx[:, :m].contiguous()
 
 
