@@ -801,6 +801,14 @@ __global__ __launch_bounds__(1024) void chamfer_cull_prep_kernel(const float *__
   if (tid == 0) ws.flag[b * 2 + c] = bad;
 }
 
+// float -> int preserving order (NaN aside): non-negative floats keep their bits, negative ones
+// have the magnitude bits flipped
+__device__ __forceinline__ int ford(float f) {
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float ford_inv(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
+
 __device__ __forceinline__ float box_gap(float qlo, float qhi, float tlo, float thi) {
   return fmaxf(0.f, fmaxf(tlo - qhi, qlo - thi));
 }
@@ -808,6 +816,9 @@ __device__ __forceinline__ float box_gap(float qlo, float qhi, float tlo, float 
 // grid (blocks of dir 0 + blocks of dir 1, B), kCullQB threads: one sorted query per lane.  Each
 // wave is an independent searcher over its 64 queries (its own box, bounds, tile buffer and
 // skip decisions): no block barriers, and a 64-query box is ~4x tighter than a block's.
+#ifndef PCOPS_CULL_UNR
+#define PCOPS_CULL_UNR 4  // pass-1 screen loop unroll (x 2 points): 4 measured 1-2 % faster than 2 and 8 (r5)
+#endif
 #ifndef PCOPS_CULL_WPE
 #define PCOPS_CULL_WPE 7  // occupancy hint: 72 VGPRs, 7 waves / SIMD (LDS allows 7 blocks / CU); A/B builds override
 #endif
@@ -863,26 +874,26 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
       L[i] = bad ? -INFINITY : fminf((gx * gx + gy * gy) + gz * gz, FLT_MAX) * (1.f - 64.f * kU);
     }
   }
-  // take the untaken tile of smallest bound (first tile on equal bounds): nearest-first order
+  // take the untaken tile of smallest bound (nearest-first order; which of several equal bounds
+  // is taken first changes neither the result nor the culling's soundness).  The wave argmin is
+  // DPP (float bits mapped to a monotone int) + a ballot: the ds_bpermute form (12 dependent LDS
+  // round trips per tile, with the mb maximum below) cost more than the tile's 64-pair screen.
   auto take = [&](float &m, int &t) {
-    m = INFINITY;
+    float lm = INFINITY;
     int mi = 0;
 #pragma unroll
     for (int i = 0; i < kLbRegs; ++i)
-      if (L[i] < m) m = L[i], mi = i;
-    t = lane + 64 * mi;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const float om = __shfl_xor(m, o);
-      const int ot = __shfl_xor(t, o);
-      if (om < m || (om == m && ot < t)) m = om, t = ot;
-    }
-    m = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
-    t = __builtin_amdgcn_readfirstlane(t);
-    if (lane == (t & 63)) {
+      if (L[i] < lm) lm = L[i], mi = i;
+    const int key = ford(lm);
+    const int kmin = wave_min_i32_dpp(key);                 // uniform
+    const int wl = (int)__builtin_ctzll(__ballot(key == kmin));
+    const int wmi = __builtin_amdgcn_readlane(mi, wl);
+    m = ford_inv(kmin);
+    t = wl + 64 * wmi;
+    if (lane == wl) {
 #pragma unroll
       for (int i = 0; i < kLbRegs; ++i)
-        if (i == (t >> 6)) L[i] = INFINITY;
+        if (i == wmi) L[i] = INFINITY;
     }
   };
   auto fetch = [&](float m, int t) {  // the tile's points, one per lane (issued a tile ahead)
@@ -933,7 +944,7 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
     __builtin_amdgcn_wave_barrier();
     float mt = INFINITY;
     if (ES) {
-#pragma unroll 2
+#pragma unroll PCOPS_CULL_UNR
       for (int kk = 0; kk < kCullTS; kk += 2) {
         const float4 p0 = tile[kk], p1 = tile[kk + 1];
         const float e0 = __builtin_fmaf(mz, p0.z, __builtin_fmaf(my, p0.y, __builtin_fmaf(mx, p0.x, p0.w)));
@@ -976,7 +987,7 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
       else if (mt == best)
         tie = true;
     }
-    mb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_max_f32(valid ? best : -INFINITY))));
+    mb = ford_inv(wave_max_i32(ford(valid ? best : -INFINITY)));   // DPP, uniform
   }
   if (!valid) return;
   int bidx = INT_MAX;
