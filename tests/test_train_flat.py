@@ -389,3 +389,34 @@ def test_flat_adam_matches_torch_fused(kind, bf16_grads):
     torch.testing.assert_close(sb["exp_avg"], sa["exp_avg"], rtol=2e-6, atol=1e-10)
     torch.testing.assert_close(sb["exp_avg_sq"], sa["exp_avg_sq"], rtol=2e-6, atol=1e-14)
     assert torch.equal(fb.flat16, fb.flat[:fb.n16].to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+def test_flat_adam_validates_state_and_lr():
+    """FlatAdam hands the kernel raw pointers to the step counter and a tensor LR: a step
+    kept as a Python number or a host / float64 tensor (a non-capturable optimizer, an old checkpoint)
+    is converted to a device fp32 tensor before use; a tensor LR that is not a 0-dim fp32 tensor on the
+    master's device is refused; Adam(decoupled_weight_decay=True) takes the AdamW update."""
+    from svdformer_pointsea_amd.train import FlatAdam
+
+    dev = "cuda"
+    torch.manual_seed(5)
+    fp = FlatParams(_NetMix().to(dev), dev)
+    with pytest.raises(ValueError, match="tensor lr"):
+        FlatAdam(torch.optim.Adam([fp.master()], lr=torch.tensor(1e-3), fused=True), fp)        # host LR
+    with pytest.raises(ValueError, match="tensor lr"):
+        FlatAdam(torch.optim.Adam([fp.master()], lr=torch.tensor(1e-3, dtype=torch.float64, device=dev),
+                                  capturable=True), fp)
+    opt = torch.optim.Adam([fp.master()], lr=1e-3, decoupled_weight_decay=True, weight_decay=1e-2)
+    flat = FlatAdam(opt, fp)
+    assert flat.adamw
+    p = fp.master()
+    for step in (3, torch.tensor(3.0), torch.tensor(3.0, dtype=torch.float64)):
+        opt.state[p] = {"step": step, "exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
+        x = torch.randn(8, 37, device=dev)
+        fp.zero_grad()
+        fp.forward(x).backward()
+        fp.collect()
+        flat.step(bf16_grads=False)
+        st = opt.state[p]["step"]
+        assert st.is_cuda and st.dtype == torch.float32 and float(st) == 4.0
