@@ -414,8 +414,10 @@ def test_flat_adam_validates_state_and_lr():
     for step in (3, torch.tensor(3.0), torch.tensor(3.0, dtype=torch.float64)):
         opt.state[p] = {"step": step, "exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
         x = torch.randn(8, 37, device=dev)
-        fp.zero_grad()
-        fp.forward(x).backward()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            fp.zero_grad()
+            fp.refresh()
+            fp.forward(x).backward()
         fp.collect()
         flat.step(bf16_grads=False)
         st = opt.state[p]["step"]
