@@ -207,6 +207,8 @@ def test_model_step_capture_replays(dev, monkeypatch, model_name):
                 assert err <= 0.05 * float(r.abs().max()) + 1e-8, (name, rep, err)
             else:
                 # within 4x the eager run-to-run spread of that gradient (MIOpen's conv weight
-                # gradients vary by ~1e-3 run to run) plus 1e-4 of its largest magnitude
+                # gradients vary by ~1e-3 run to run) plus 1e-4 of its largest magnitude; the 1e-7
+                # floor covers gradients that are rounding noise around 0 (a conv bias right before
+                # a BatchNorm: |g| ~ 1e-8)
                 err = float((p.grad - r).abs().max())
-                assert err <= 4 * float(sp) + 1e-4 * float(r.abs().max()) + 1e-8, (name, rep, err, float(sp))
+                assert err <= 4 * float(sp) + 1e-4 * float(r.abs().max()) + 1e-7, (name, rep, err, float(sp))
