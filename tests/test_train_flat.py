@@ -410,7 +410,7 @@ def test_flat_adam_validates_state_and_lr():
     opt = torch.optim.Adam([fp.master()], lr=1e-3, decoupled_weight_decay=True, weight_decay=1e-2)
     flat = FlatAdam(opt, fp)
     assert flat.adamw
-    p = fp.master()
+    p = opt.param_groups[0]["params"][0]   # the optimizer's own key (master() returns a new view)
     for step in (3, torch.tensor(3.0), torch.tensor(3.0, dtype=torch.float64)):
         opt.state[p] = {"step": step, "exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
         x = torch.randn(8, 37, device=dev)
