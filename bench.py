@@ -84,7 +84,7 @@ def parse():
                     help="with --gpus N > 1 outside torch.distributed.run: print the rank launcher's argv and exit")
     ap.add_argument("--pmc-attn-json", default=os.path.join(ROOT, "profiles", "r4_pmc_attn.json"),
                     help="attention MFMA counters (tools/pmc_attn.py) -> attention.pmc_mfma_util")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r4_pmc_traffic.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r5_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
     return ap.parse_args()
