@@ -189,6 +189,10 @@ __global__ __launch_bounds__(kThreads) void chamfer_nn_kernel(const float *__res
 // keep / prune test below allows.  A query whose slots overflow (near-ties
 // across > 4 sub-tiles) or is not finite is re-derived by a full direct scan.
 constexpr int kSlots = 4;
+#ifndef PCOPS_CH_RD
+#define PCOPS_CH_RD 8  // re-derivation: candidate targets loaded per batch (A/B builds override)
+#endif
+constexpr int kRd = PCOPS_CH_RD;
 constexpr float kU = 5.9604645e-8f;  // 2^-24
 
 __device__ __forceinline__ float screen_slack(float mine, float an, float eps) {
@@ -330,11 +334,26 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
       for (int c = 0; c < kSlots; ++c) {
         if (cs[i][c] < 0) continue;
         const int k0 = cs[i][c], k1 = min(k0 + kSub, NT);
-        for (int k = k0; k < k1; ++k) {
-          const float d = sqd3(T[3 * k] - ax[i], T[3 * k + 1] - ay[i], T[3 * k + 2] - az[i]);
-          if (d < best || (d == best && k < bk)) {
-            best = d;
-            bk = k;
+        // the candidate targets' coordinates in batches of kRd, every batch's loads issued
+        // together (the plain loop waited out one global-load latency per target: most of
+        // this kernel's time at the small launches, where it is not hidden by other waves)
+        for (int kb = k0; kb < k1; kb += kRd) {
+          float px[kRd], py[kRd], pz[kRd];
+#pragma unroll
+          for (int j = 0; j < kRd; ++j) {
+            const int kc = min(kb + j, k1 - 1);
+            px[j] = T[3 * kc];
+            py[j] = T[3 * kc + 1];
+            pz[j] = T[3 * kc + 2];
+          }
+#pragma unroll
+          for (int j = 0; j < kRd; ++j) {
+            const int k = kb + j;
+            const float d = sqd3(px[j] - ax[i], py[j] - ay[i], pz[j] - az[i]);
+            if (k < k1 && (d < best || (d == best && k < bk))) {
+              best = d;
+              bk = k;
+            }
           }
         }
       }
@@ -991,12 +1010,18 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
   }
   if (!valid) return;
   int bidx = INT_MAX;
-  auto scan_tile = [&](int u) {
-    for (int k = u * kCullTS, ke = min(NT, k + kCullTS); k < ke; ++k) {
-      const float4 p = T[k];
-      const float d = sqd3(p.x - a.x, p.y - a.y, p.z - a.z);
-      const int ti = __float_as_int(p.w);
-      if (d < best || (d == best && ti < bidx)) best = d, bidx = ti;
+  auto scan_tile = [&](int u) {   // the tile's sorted rows in batches of kRd loads issued together
+    const int ke = min(NT, u * kCullTS + kCullTS);
+    for (int kb = u * kCullTS; kb < ke; kb += kRd) {
+      float4 pr[kRd];
+#pragma unroll
+      for (int j = 0; j < kRd; ++j) pr[j] = T[min(kb + j, ke - 1)];
+#pragma unroll
+      for (int j = 0; j < kRd; ++j) {
+        const float d = sqd3(pr[j].x - a.x, pr[j].y - a.y, pr[j].z - a.z);
+        const int ti = __float_as_int(pr[j].w);
+        if (kb + j < ke && (d < best || (d == best && ti < bidx))) best = d, bidx = ti;
+      }
     }
   };
   // every tile whose box is within `bound` (all of them in a non-finite batch)

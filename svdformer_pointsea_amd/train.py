@@ -265,6 +265,11 @@ class FlatAdam:
         elif not torch.cuda.is_current_stream_capturing():
             self._check_state()   # a state loaded since (load_state_dict) is validated before use
         st["step"].add_(1)
+        # this IS the optimizer's step (its own step() is never called): flag it the way the LR
+        # scheduler's wrapper of opt.step does, so the schedule does not take a batch_end() after
+        # it for the "scheduler before optimizer" misuse (the LR sequence is pinned by
+        # tests/test_train_flat.py::test_captured_flat_adam_follows_lr_schedule)
+        self.opt._opt_called = True
         lr = g["lr"]
         lr_dev = lr if isinstance(lr, torch.Tensor) else None
         fp = self.fp

@@ -422,3 +422,67 @@ def test_flat_adam_validates_state_and_lr():
         flat.step(bf16_grads=False)
         st = opt.state[p]["step"]
         assert st.is_cuda and st.dtype == torch.float32 and float(st) == 4.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["svdformer", "pointsea"])
+def test_captured_flat_adam_follows_lr_schedule(model):
+    """bench.py's optimizer path (VERDICT r4 hygiene): FlatAdam over a fused capturable Adam (PCN) /
+    AdamW (ShapeNet-55) whose LR is a device tensor, the update captured ONCE into a HIP graph and
+    replayed, TrainSchedule.batch_end() between replays (epoch_end every 7 batches, as the golden's
+    loop).  Before replay i the LR tensor the graph reads holds golden[i] (the reference's
+    GradualWarmupScheduler sequence, tests/golden/make_golden_train.py) to fp32 rounding -- the
+    schedule does its arithmetic on the fp32 device tensor -- and after it the master weights equal,
+    bitwise, an eager FlatAdam handed that same value as a host number: the graph applies the live
+    LR, not the one at capture.  No scheduler warning is raised (FlatAdam flags its step as the
+    optimizer's)."""
+    import warnings
+
+    import numpy as np
+
+    from conftest import golden
+    from svdformer_pointsea_amd.train import FlatAdam, TrainSchedule
+
+    dev = "cuda"
+    gold = golden("lr_schedule.npz")["pcn" if model == "svdformer" else "55"]
+    torch.manual_seed(11)
+    a = _NetMix().to(dev)
+    b = copy.deepcopy(a)
+    fa, fb = FlatParams(a, dev), FlatParams(b, dev)
+    mk = (lambda ps, lr: torch.optim.Adam(ps, lr=lr, betas=(0.9, 0.999), weight_decay=0, fused=True,
+                                          capturable=True)) if model == "svdformer" else \
+         (lambda ps, lr: torch.optim.AdamW(ps, lr=lr, weight_decay=0.0005, fused=True, capturable=True))
+    lr_t = torch.tensor(1e-4, device=dev)
+    oa, ob = mk([fa.master()], lr_t), mk([fb.master()], 1e-4)
+    fla, flb = FlatAdam(oa, fa), FlatAdam(ob, fb)
+    fa.refresh()
+    fb.refresh()
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for f in (fa, fb):   # one fixed gradient (bf16 shadow region + fp32 region), the same on both
+        f.grad16.copy_(torch.randn(f.grad16.shape, generator=gen.manual_seed(3), device=dev))
+        f.grad.copy_(torch.randn(f.grad.shape, generator=gen.manual_seed(4), device=dev))
+    graph = None
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        sch = TrainSchedule(oa, model)
+        for i, want in enumerate(gold):
+            lr_now = float(oa.param_groups[0]["lr"])
+            assert oa.param_groups[0]["lr"] is lr_t
+            # fp32 rounding, compounded over StepLR's per-epoch x0.98 (measured worst 8e-7 on the CPU)
+            np.testing.assert_allclose(lr_now, want, rtol=2e-6, atol=0, err_msg=f"batch {i}")
+            if graph is None:     # the first update eagerly (creates the state), then captured once
+                fla.step()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    fla.step()
+            else:
+                graph.replay()
+            ob.param_groups[0]["lr"] = lr_now
+            flb.step()
+            sch.batch_end()
+            if (i + 1) % 7 == 0:
+                sch.epoch_end()
+            assert torch.equal(fa.flat, fb.flat), f"batch {i}: master differs (lr {lr_now})"
+    assert torch.equal(fa.flat16, fb.flat16)
+    bad = [str(w.message) for w in caught if "lr_scheduler" in str(w.message) or "optimizer.step" in str(w.message)]
+    assert not bad, bad
