@@ -531,6 +531,7 @@ class SDG(nn.Module):
 # PCOPS_IMG_STREAM=1: the image branch on a third stream beside the point branch.  Off: same-box PCN
 # A/B, 5 runs each, 51.01-53.04 ms (mean 52.1, bimodal run to run) against 51.64-51.91 (mean 51.78)
 _IMG_STREAM = _os.environ.get("PCOPS_IMG_STREAM", "0") == "1"
+_IMG_FIRST = _os.environ.get("PCOPS_IMG_FIRST", "0") == "1"
 
 
 class _NoFork:
@@ -572,17 +573,24 @@ class SVFNet(nn.Module):
         self.register_buffer("view_point", torch.tensor([0, 0, -d, -d, 0, 0, 0, d, 0], dtype=torch.float32)
                              .view(-1, 3, 3).permute(0, 2, 1).contiguous(), persistent=False)
 
-    def forward(self, points, depth, fidx=None):
-        batch_size, _, N = points.size()
+    def image_features(self, depth, batch_size):
+        """The image branch: (3B, 1, 224, 224) depth images -> (B, 256, 3) view features."""
         depth = depth.contiguous(memory_format=torch.channels_last)
+        # stem conv (1 -> 16) on libpcops under bf16 autocast, each BN + ReLU fused
+        f_v = run_sequential(self.img_feature_extractor, depth, conv3x3).view(batch_size, 3, -1).transpose(1, 2)
+        return f_v.contiguous()
+
+    def forward(self, points, depth, fidx=None, f_v=None):
+        """f_v: the image branch's output when the caller already issued it (image_features)."""
+        batch_size, _, N = points.size()
         # the image branch (convs + BatchNorm, no GEMM) and the point branch (FPS, kNN, grouping,
         # PCSA: launches of 32-512 blocks) are independent until viewattn: with PCOPS_IMG_STREAM
         # the image branch runs on a third stream beside the point branch (and the local
         # encoder on the first side stream), forward and backward
-        with fork(points.device, lane=2, inputs=(depth,)) if _IMG_STREAM else _NoFork() as br:
-            # stem conv (1 -> 16) on libpcops under bf16 autocast, each BN + ReLU fused
-            f_v = run_sequential(self.img_feature_extractor, depth, conv3x3).view(batch_size, 3, -1).transpose(1, 2)
-            f_v = f_v.contiguous()
+        br = _NoFork()
+        if f_v is None:
+            with fork(points.device, lane=2, inputs=(depth,)) if _IMG_STREAM else _NoFork() as br:
+                f_v = self.image_features(depth, batch_size)
         f_p = self.point_feature_extractor(points, fidx=fidx)
         f_v = br.join(f_v)
         view_point = self.view_point.expand(batch_size, 3, 3)
@@ -646,6 +654,9 @@ class Model(nn.Module):
 
     def forward(self, partial, depth):
         partial_cm = partial.transpose(1, 2).contiguous()
+        # PCOPS_IMG_FIRST=1: the image branch issued before the local-encoder fork (A/B of the
+        # order the captured graph's nodes are created in)
+        f_v = self.encoder.image_features(depth, partial.shape[0]) if _IMG_FIRST else None
         # the local encoder (EdgeConv kNN, FPS, 1x1-conv GEMMs on rocBLAS: no stream-K)
         # only depends on the partial cloud: it runs on a second HIP stream
         # beside the view/point encoder
@@ -656,7 +667,7 @@ class Model(nn.Module):
             fidx = shared_partial_fps(partial, self.localencoder.local_number,
                                       self.encoder.point_feature_extractor.sa_module_1.npoint)
             local_feat = self.localencoder(partial_cm, fidx=fidx)
-        feat_g, coarse = self.encoder(partial_cm, depth, fidx=fidx)
+        feat_g, coarse = self.encoder(partial_cm, depth, fidx=fidx, f_v=f_v)
         local_feat = br.join(local_feat)
         coarse_merge = torch.cat([partial_cm, coarse.to(partial_cm.dtype)], dim=2).float().contiguous()
         coarse_merge = gather_operation(coarse_merge, furthest_point_sample(coarse_merge.transpose(1, 2).contiguous(),

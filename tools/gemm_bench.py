@@ -28,7 +28,7 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
-T = 65536
+T = int(os.environ.get('GEMM_T', 65536))
 for (cin, cout) in [(512, 1536), (512, 512), (512, 1024), (1024, 512), (1024, 3072), (1024, 1024), (768, 2304)]:
     x = torch.randn(T, cin, device=dev, dtype=torch.bfloat16)
     w = torch.randn(cout, cin, device=dev, dtype=torch.bfloat16)
@@ -45,6 +45,9 @@ for (cin, cout) in [(512, 1536), (512, 512), (512, 1024), (1024, 512), (1024, 30
         xb = x.view(S, T // S, cin)
         ws = timeit(lambda: torch.bmm(gb, xb, out_dtype=torch.float32).sum(0).to(torch.bfloat16))
         line += f" | splitK{S} {ws*1e3:.0f}us {fl/ws/1e9:.0f}TF"
+    from svdformer_pointsea_amd.attention import _wgrad
+    wp = timeit(lambda: _wgrad(g, x, torch.bfloat16))
+    line += f" | product _wgrad {wp*1e3:.0f}us {fl/wp/1e9:.0f}TF"
     ref = (g.t().float() @ x.float())
     err = (torch.bmm(g.view(8, T // 8, cout).transpose(1, 2), x.view(8, T // 8, cin), out_dtype=torch.float32).sum(0)
            - ref).abs().max().item()
