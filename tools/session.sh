@@ -1,18 +1,9 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r5kq; mkdir -p $O
-for r in 1 2 3; do
-  for kp in 0 16777216 67108864; do
-    if [ $kp = 0 ]; then E="X=0"; else E="HSA_KERNARG_POOL_SIZE=$kp"; fi
-    echo "== $E" >> $O/ab.txt
-    env $E timeout -k 10 300 python bench.py --no-cpu-baseline --no-fp32-leg --no-extra-legs --no-kernel-timing --steps 30 --warmup 3 >> $O/ab.txt 2>> $O/ab.err || exit 1
-  done
+O=gpurun_out/r5wh; mkdir -p $O; export TMPDIR=/tmp
+for v in "PCOPS_WGRAD_BM=128 PCOPS_WGRAD_WGS=512" "PCOPS_WGRAD_BM=256 PCOPS_WGRAD_WGS=256" "PCOPS_WGRAD_BM=256 PCOPS_WGRAD_WGS=512" "PCOPS_WGRAD_BM=128 PCOPS_WGRAD_WGS=1024"; do
+  echo "== $v" >> $O/ab.txt
+  env $v PCOPS_WGRAD_MFMA=1 timeout -k 10 200 python tools/gemm_bench.py tuned 2>&1 | grep -o "^[0-9]*->[0-9]*\|product _wgrad [0-9]*us [0-9]*TF" | paste - - >> $O/ab.txt || exit 1
 done
-python - <<'PY'
-import json
-for l in open('gpurun_out/r5kq/ab.txt'):
-    if l.startswith('=='): print(l.strip(), end=' ')
-    elif l.startswith('{'):
-        d=json.loads(l); print(round(d['ms_per_step'],2), 'host', round(d.get('host_issue_ms_per_step',0),2))
-PY
+cat $O/ab.txt
