@@ -18,6 +18,7 @@
 // torch runs the same BasicBlock as MIOpen mean/variance + norm + clamp + add
 // forward and threshold_backward + dscale/dbias + dx (+ autograd's adds)
 // backward: 3 and 4-5 launches, each a full pass over the activation.
+#include <atomic>
 #include <cstdlib>
 
 #include "common.h"
@@ -122,14 +123,77 @@ __device__ __forceinline__ void bn_accum(const void *__restrict__ x, const void 
   }
 }
 
-template <int DT, int MODE>
+// what the final step writes (forward: statistics, running stats, scale / shift; backward: dgamma,
+// dbeta and the dx coefficients)
+struct BnFin {
+  const void *x;
+  const float *gamma, *beta;
+  float *rmean, *rvar;
+  float momentum, eps;
+  float *mean_io, *invstd_io, *dgamma, *dbeta;
+  int eval;
+  float *coef;
+  long long *nbt;
+  long long rows;
+  int C;
+};
+
+// channel c's final from its combined sums s0, s1 (double)
+template <int MODE, int DT>
+__device__ __forceinline__ void bn_final_col(int c, double s0, double s1, const BnFin &f) {
+  const int C = f.C;
+  const double n = (double)f.rows;
+  const double g = f.gamma ? (double)f.gamma[c] : 1.0;
+  if constexpr (MODE == 0) {
+    const double k = DT == 0 ? (double)reinterpret_cast<const float *>(f.x)[c]
+                             : (double)(float)reinterpret_cast<const __bf16 *>(f.x)[c];
+    const double m1 = s0 / n;
+    double var = s1 / n - m1 * m1;
+    if (var < 0.0) var = 0.0;
+    const double mean = k + m1;
+    const float invstd = 1.0f / sqrtf((float)var + f.eps);  // torch: 1 / sqrt(var + eps) in fp32
+    f.mean_io[c] = (float)mean;
+    f.invstd_io[c] = invstd;
+    if (f.rmean) {
+      f.rmean[c] = (float)(f.momentum * mean + (1.0 - f.momentum) * (double)f.rmean[c]);
+      const double unbiased = f.rows > 1 ? var * n / (n - 1.0) : var;
+      f.rvar[c] = (float)(f.momentum * unbiased + (1.0 - f.momentum) * (double)f.rvar[c]);
+    }
+    if (f.nbt && c == 0) f.nbt[0] += 1;  // module.num_batches_tracked (no separate add launch)
+    const double sc = g * (double)invstd;
+    f.coef[c] = (float)sc;
+    f.coef[C + c] = (float)((f.beta ? (double)f.beta[c] : 0.0) - (double)(float)mean * sc);
+  } else {
+    const double inv = (double)f.invstd_io[c];
+    if (f.dgamma) f.dgamma[c] = (float)(s1 * inv);
+    if (f.dbeta) f.dbeta[c] = (float)s0;
+    const double ca = g * inv;
+    double cb = 0.0, cc = 0.0;
+    if (!f.eval) {
+      cb = -g * inv * inv * inv * s1 / n;
+      cc = -ca * s0 / n - cb * (double)f.mean_io[c];
+    }
+    f.coef[c] = (float)ca;
+    f.coef[C + c] = (float)cb;
+    f.coef[2 * C + c] = (float)cc;
+  }
+}
+
+// Arrival counters of the fused final (bn_partial_kernel<.., FUSE = true>): zero at load; every
+// launch takes its own `strips` slots (bn_arrive_slots) and the last arriving block of a strip
+// resets its slot, so a captured graph replays with every slot back at zero.
+constexpr unsigned kBnSlots = 1u << 16;
+__device__ unsigned g_bn_arrive[kBnSlots];
+
+template <int DT, int MODE, bool FUSE>
 __global__ __launch_bounds__(64 * kBnWaves) void bn_partial_kernel(const void *__restrict__ x,
                                                                    const void *__restrict__ dy,
                                                                    const void *__restrict__ y,
                                                                    const float *__restrict__ mean, long long rows,
                                                                    int C, int V, long long rpc, float slope,
-                                                                   float *__restrict__ part) {
-  extern __shared__ float red[];  // [kBnWaves][2][V*8]
+                                                                   float *__restrict__ part, BnFin fin,
+                                                                   unsigned slot) {
+  extern __shared__ float red[];  // [kBnWaves][2][V*8]; FUSE: also the final's [2][16][V*8] doubles
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rw = 64 / V;
   const int rsub = lane / V, vi = lane - rsub * V;
@@ -175,7 +239,62 @@ __global__ __launch_bounds__(64 * kBnWaves) void bn_partial_kernel(const void *_
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < kBnWaves; ++q) s += red[(q * 2 + h) * W8 + c];
-    part[(long long)blockIdx.x * 2 * C + h * C + blockIdx.y * W8 + c] = s;
+    float *dst = part + (long long)blockIdx.x * 2 * C + h * C + blockIdx.y * W8 + c;
+    if constexpr (FUSE)
+      __hip_atomic_store(dst, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: written through
+    else
+      *dst = s;
+  }
+  if constexpr (FUSE) {
+    // The strip's last block to finish runs bn_final_kernel's step for the strip's W8 channels, in
+    // the same order (16 chunk groups summed in double, then the groups in order): one launch less.
+    // Hand-off without an L2 write-back (a __threadfence() per block cost more than the launch it
+    // saved): the partial rows are stored sc1 (write-through), every storing wave drains its stores,
+    // one lane per block counts the block in with an agent-scope add, and the block whose add came
+    // last reads every partial with sc1 loads.
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(&g_bn_arrive[slot + blockIdx.y], 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    const int chunks = gridDim.x;
+    double *dred = reinterpret_cast<double *>(red);   // [2][16][W8]
+    for (int pi = threadIdx.x; pi < 16 * W8; pi += 64 * kBnWaves) {
+      const int grp = pi / W8, cj = pi - grp * W8, c = blockIdx.y * W8 + cj;
+      float pa[16], pb[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k = grp + 16 * i;
+        pa[i] = k < chunks ? __hip_atomic_load(part + (long long)k * 2 * C + c, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.f;
+        pb[i] = k < chunks ? __hip_atomic_load(part + (long long)k * 2 * C + C + c, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.f;
+      }
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        a += (double)pa[i];
+        b += (double)pb[i];
+      }
+      dred[grp * W8 + cj] = a;
+      dred[(16 + grp) * W8 + cj] = b;
+    }
+    __syncthreads();
+    for (int cj = threadIdx.x; cj < W8; cj += 64 * kBnWaves) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int i = 0; i < 16; ++i) {
+        s0 += dred[i * W8 + cj];
+        s1 += dred[(16 + i) * W8 + cj];
+      }
+      bn_final_col<MODE == 0 ? 0 : 1, DT>(blockIdx.y * W8 + cj, s0, s1, fin);
+    }
+    if (threadIdx.x == 0)   // back to zero for the next launch that draws this slot
+      __hip_atomic_store(&g_bn_arrive[slot + blockIdx.y], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -185,16 +304,9 @@ __global__ __launch_bounds__(64 * kBnWaves) void bn_partial_kernel(const void *_
 // MODE 1: backward -> dgamma, dbeta, coef = (a, b, c) with dx = a g + b x + c
 //         (batch statistics: the full BN gradient; `eval` = 1: running statistics, dx = a g)
 template <int MODE, int DT>
-__global__ __launch_bounds__(512) void bn_final_kernel(const float *__restrict__ part, int chunks, int C,
-                                                       long long rows, const void *__restrict__ x,
-                                                       const float *__restrict__ gamma,
-                                                       const float *__restrict__ beta, float *__restrict__ rmean,
-                                                       float *__restrict__ rvar, float momentum, float eps,
-                                                       float *__restrict__ mean_io, float *__restrict__ invstd_io,
-                                                       float *__restrict__ dgamma, float *__restrict__ dbeta,
-                                                       int eval, float *__restrict__ coef,
-                                                       long long *__restrict__ nbt) {
+__global__ __launch_bounds__(512) void bn_final_kernel(const float *__restrict__ part, int chunks, BnFin fin) {
   __shared__ double red[2][16][33];
+  const int C = fin.C;
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   double a = 0.0, b = 0.0;
@@ -222,41 +334,7 @@ __global__ __launch_bounds__(512) void bn_final_kernel(const float *__restrict__
     s0 += red[0][i][cl];
     s1 += red[1][i][cl];
   }
-  const double n = (double)rows;
-  const double g = gamma ? (double)gamma[c] : 1.0;
-  if constexpr (MODE == 0) {
-    const double k = DT == 0 ? (double)reinterpret_cast<const float *>(x)[c]
-                             : (double)(float)reinterpret_cast<const __bf16 *>(x)[c];
-    const double m1 = s0 / n;
-    double var = s1 / n - m1 * m1;
-    if (var < 0.0) var = 0.0;
-    const double mean = k + m1;
-    const float invstd = 1.0f / sqrtf((float)var + eps);  // torch: 1 / sqrt(var + eps) in fp32
-    mean_io[c] = (float)mean;
-    invstd_io[c] = invstd;
-    if (rmean) {
-      rmean[c] = (float)(momentum * mean + (1.0 - momentum) * (double)rmean[c]);
-      const double unbiased = rows > 1 ? var * n / (n - 1.0) : var;
-      rvar[c] = (float)(momentum * unbiased + (1.0 - momentum) * (double)rvar[c]);
-    }
-    if (nbt && c == 0) nbt[0] += 1;  // module.num_batches_tracked (no separate add launch)
-    const double sc = g * (double)invstd;
-    coef[c] = (float)sc;
-    coef[C + c] = (float)((beta ? (double)beta[c] : 0.0) - (double)(float)mean * sc);
-  } else {
-    const double inv = (double)invstd_io[c];
-    if (dgamma) dgamma[c] = (float)(s1 * inv);
-    if (dbeta) dbeta[c] = (float)s0;
-    const double ca = g * inv;
-    double cb = 0.0, cc = 0.0;
-    if (!eval) {
-      cb = -g * inv * inv * inv * s1 / n;
-      cc = -ca * s0 / n - cb * (double)mean_io[c];
-    }
-    coef[c] = (float)ca;
-    coef[C + c] = (float)cb;
-    coef[2 * C + c] = (float)cc;
-  }
+  bn_final_col<MODE, DT>(c, s0, s1, fin);
 }
 
 // eval-mode forward coefficients from the running statistics
@@ -334,18 +412,48 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const void *__restric
   }
 }
 
-template <int DT>
-void launch_partial(int mode, const void *x, const void *dy, const void *y, const float *mean, long long rows, int C,
-                    float slope, float *part, int chunks, long long rpc, hipStream_t s) {
+// the fused final (PCOPS_BN_FUSED_FINAL, default on; read per call so a test can compare both forms)
+// for strips of <= 128 channels: its [2][16][W8] double image fits the block's LDS
+bool bn_fuse(int C) {
+  const char *e = getenv("PCOPS_BN_FUSED_FINAL");
+  return (!e || atoi(e) != 0) && bn_v(C) * 8 <= 128;
+}
+
+unsigned bn_arrive_slots(int n) {   // host side: `n` consecutive counters no other launch in flight holds
+  static std::atomic<unsigned> next{0};
+  unsigned b = next.fetch_add((unsigned)n) % kBnSlots;
+  if (b + (unsigned)n > kBnSlots) b = 0;
+  return b;
+}
+
+template <int DT, bool FUSE>
+void launch_partial_t(int mode, const void *x, const void *dy, const void *y, const float *mean, long long rows, int C,
+                      float slope, float *part, int chunks, long long rpc, const BnFin &fin, hipStream_t s) {
   const int V = bn_v(C);
   const dim3 grid(chunks, C / 8 / V), block(64 * kBnWaves);
-  const size_t lds = (size_t)kBnWaves * 2 * V * 8 * sizeof(float);
+  const size_t lds = FUSE ? (size_t)2 * 16 * V * 8 * sizeof(double) : (size_t)kBnWaves * 2 * V * 8 * sizeof(float);
+  const unsigned slot = FUSE ? bn_arrive_slots(C / 8 / V) : 0u;
   switch (mode) {
-    case 0: hipLaunchKernelGGL((bn_partial_kernel<DT, 0>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part); break;
-    case 1: hipLaunchKernelGGL((bn_partial_kernel<DT, 1>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part); break;
-    case 2: hipLaunchKernelGGL((bn_partial_kernel<DT, 2>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part); break;
-    default: hipLaunchKernelGGL((bn_partial_kernel<DT, 3>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part); break;
+    case 0: hipLaunchKernelGGL((bn_partial_kernel<DT, 0, FUSE>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part, fin, slot); break;
+    case 1: hipLaunchKernelGGL((bn_partial_kernel<DT, 1, FUSE>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part, fin, slot); break;
+    case 2: hipLaunchKernelGGL((bn_partial_kernel<DT, 2, FUSE>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part, fin, slot); break;
+    default: hipLaunchKernelGGL((bn_partial_kernel<DT, 3, FUSE>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part, fin, slot); break;
   }
+}
+
+// partial sums + final: one launch (fused) or two
+template <int DT>
+void launch_stats(int mode, const void *x, const void *dy, const void *y, const float *mean, long long rows, int C,
+                  float slope, float *part, int chunks, long long rpc, const BnFin &fin, hipStream_t s) {
+  if (bn_fuse(C)) {
+    launch_partial_t<DT, true>(mode, x, dy, y, mean, rows, C, slope, part, chunks, rpc, fin, s);
+    return;
+  }
+  launch_partial_t<DT, false>(mode, x, dy, y, mean, rows, C, slope, part, chunks, rpc, fin, s);
+  if (mode == 0)
+    hipLaunchKernelGGL((bn_final_kernel<0, DT>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, fin);
+  else
+    hipLaunchKernelGGL((bn_final_kernel<1, DT>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, fin);
 }
 
 template <int DT, int RT>
@@ -409,17 +517,13 @@ extern "C" int pcops_batchnorm_fwd(const void *x, int dtype, const void *res, in
   float *part = (float *)workspace;
   float *coef = part + (long long)chunks * 2 * C;
   if (batch_stats) {
-    if (dtype == 0) {
-      launch_partial<0>(0, x, nullptr, nullptr, nullptr, rows, C, 0.f, part, chunks, rpc, s);
-      hipLaunchKernelGGL((bn_final_kernel<0, 0>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
-                         gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, nullptr,
-                         nullptr, 0, coef, running_mean ? num_batches_tracked : nullptr);
-    } else {
-      launch_partial<1>(0, x, nullptr, nullptr, nullptr, rows, C, 0.f, part, chunks, rpc, s);
-      hipLaunchKernelGGL((bn_final_kernel<0, 1>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
-                         gamma, beta, running_mean, running_var, momentum, eps, save_mean, save_invstd, nullptr,
-                         nullptr, 0, coef, running_mean ? num_batches_tracked : nullptr);
-    }
+    BnFin fin{x,         gamma,   beta,    running_mean, running_var, momentum,
+              eps,       save_mean, save_invstd, nullptr, nullptr,     0,
+              coef,      running_mean ? num_batches_tracked : nullptr, rows, C};
+    if (dtype == 0)
+      launch_stats<0>(0, x, nullptr, nullptr, nullptr, rows, C, 0.f, part, chunks, rpc, fin, s);
+    else
+      launch_stats<1>(0, x, nullptr, nullptr, nullptr, rows, C, 0.f, part, chunks, rpc, fin, s);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, running_mean,
                        running_var, eps, save_mean, save_invstd, coef);
@@ -461,17 +565,12 @@ extern "C" int pcops_batchnorm_bwd(const void *dy, const void *y, const void *x,
   float *part = (float *)workspace;
   float *coef = part + (long long)chunks * 2 * C;
   const int mode = 1 + act;
-  if (dtype == 0) {
-    launch_partial<0>(mode, x, dy, y, save_mean, rows, C, slope, part, chunks, rpc, s);
-    hipLaunchKernelGGL((bn_final_kernel<1, 0>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
-                       gamma, nullptr, nullptr, nullptr, 0.f, 0.f, (float *)save_mean, (float *)save_invstd, dgamma,
-                       dbeta, batch_stats ? 0 : 1, coef, nullptr);
-  } else {
-    launch_partial<1>(mode, x, dy, y, save_mean, rows, C, slope, part, chunks, rpc, s);
-    hipLaunchKernelGGL((bn_final_kernel<1, 1>), dim3((C + 31) / 32), dim3(512), 0, s, part, chunks, C, rows, x,
-                       gamma, nullptr, nullptr, nullptr, 0.f, 0.f, (float *)save_mean, (float *)save_invstd, dgamma,
-                       dbeta, batch_stats ? 0 : 1, coef, nullptr);
-  }
+  BnFin fin{x,       gamma,  nullptr, nullptr, nullptr, 0.f, 0.f, (float *)save_mean, (float *)save_invstd, dgamma,
+            dbeta,   batch_stats ? 0 : 1, coef, nullptr, rows, C};
+  if (dtype == 0)
+    launch_stats<0>(mode, x, dy, y, save_mean, rows, C, slope, part, chunks, rpc, fin, s);
+  else
+    launch_stats<1>(mode, x, dy, y, save_mean, rows, C, slope, part, chunks, rpc, fin, s);
   const unsigned n8 = (unsigned)(rows * C / 8);
   const bool r = dres != nullptr;
   if (dtype == 0) {

@@ -231,3 +231,77 @@ def test_edgeconv_fused_vs_torch(dev, monkeypatch):
         torch.testing.assert_close(ga[k], gb[k], atol=1e-3, rtol=1e-3)
     for k in ba:
         torch.testing.assert_close(ba[k], bb[k], atol=1e-5, rtol=1e-5)
+
+
+def _bn_run(dev, shape, dtype, act, res, seed):
+    g = torch.Generator().manual_seed(seed)
+    N, C, H, W = shape
+    x = (torch.randn(shape, generator=g) * 1.7 + 0.8).to(dev, dtype).contiguous(memory_format=torch.channels_last)
+    r = (torch.randn(shape, generator=g).to(dev, dtype).contiguous(memory_format=torch.channels_last)
+         if res else None)
+    dy = torch.randn(shape, generator=g).to(dev, dtype).contiguous(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+        bn.running_mean.copy_(torch.randn(C, generator=g))
+        bn.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+    xg = x.clone().requires_grad_(True)
+    rg = r.clone().requires_grad_(True) if res else None
+    y = BN.bn_act(xg, bn, act, 0.2, rg)
+    y.backward(dy)
+    out = [y, xg.grad, bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    return out + ([rg.grad] if res else [])
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 32, 32), (3, 64, 12, 12), (2, 128, 7, 9), (8, 64, 56, 56),
+                                   (2, 256, 7, 7), (5, 24, 10, 10)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_fused_final_bitwise(dev, monkeypatch, shape, dtype):
+    """The final step folded into the statistics pass (the last block of each channel strip to
+    finish combines the partial rows, PCOPS_BN_FUSED_FINAL, round 5) gives bitwise the outputs,
+    gradients and running statistics of the separate bn_final launch: the same partial rows
+    summed in the same order."""
+    for act, res in ((BN.ACT_RELU, True), (BN.ACT_LEAKY, False), (BN.ACT_NONE, False)):
+        seed = hash((shape, act, res)) % 1000
+        monkeypatch.setenv("PCOPS_BN_FUSED_FINAL", "0")
+        a = _bn_run(dev, shape, dtype, act, res, seed)
+        monkeypatch.setenv("PCOPS_BN_FUSED_FINAL", "1")
+        b = _bn_run(dev, shape, dtype, act, res, seed)
+        for i, (u, v) in enumerate(zip(a, b)):
+            assert torch.equal(u, v), (act, res, i)
+
+
+def test_bn_fused_final_graph_replays(dev):
+    """Captured once and replayed: each replay's fused launches find their arrival counters back
+    at zero (the last block resets them), so every replay equals the eager result."""
+    shape = (8, 64, 28, 28)
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(shape, generator=g) + 0.3).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(shape, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(64).to(dev)
+    xg = x.clone().requires_grad_(True)
+
+    def step():
+        xg.grad = None
+        bn.weight.grad = bn.bias.grad = None
+        y = BN.bn_act(xg, bn, BN.ACT_RELU, 0.0, None)
+        y.backward(dy)
+        return y.detach()
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        y0 = step().clone()
+        ref = [y0, xg.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone()]
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        y = step()
+    for _ in range(4):
+        graph.replay()
+        torch.cuda.synchronize()
+        got = [y, xg.grad, bn.weight.grad, bn.bias.grad]
+        for u, v in zip(ref, got):
+            assert torch.equal(u, v)

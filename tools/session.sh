@@ -1,9 +1,11 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r5wh; mkdir -p $O; export TMPDIR=/tmp
-for v in "PCOPS_WGRAD_BM=128 PCOPS_WGRAD_WGS=512" "PCOPS_WGRAD_BM=256 PCOPS_WGRAD_WGS=256" "PCOPS_WGRAD_BM=256 PCOPS_WGRAD_WGS=512" "PCOPS_WGRAD_BM=128 PCOPS_WGRAD_WGS=1024"; do
-  echo "== $v" >> $O/ab.txt
-  env $v PCOPS_WGRAD_MFMA=1 timeout -k 10 200 python tools/gemm_bench.py tuned 2>&1 | grep -o "^[0-9]*->[0-9]*\|product _wgrad [0-9]*us [0-9]*TF" | paste - - >> $O/ab.txt || exit 1
+O=gpurun_out/r5bn2; mkdir -p $O; export TMPDIR=/tmp
+for r in 1 2 3; do
+for v in 0 1; do
+  echo "== $v" >> $O/ps.txt
+  PCOPS_BN_FUSED_FINAL=$v timeout -k 10 300 python bench.py --model pointsea --no-cpu-baseline --no-fp32-leg --no-extra-legs --no-kernel-timing --steps 20 --warmup 3 >> $O/ps.txt 2>> $O/ps.err || exit 1
 done
-cat $O/ab.txt
+done
+grep -E '^==|ms_per_step' $O/ps.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
