@@ -147,3 +147,54 @@ def test_pointsea_glue_fusions_match_unfused(dev, monkeypatch):
     for n in g_a:
         err = (g_a[n].float() - g_b[n].float()).norm().item()
         assert err <= 1e-3 * g_b[n].float().norm().item() + 1e-8, (n, err)
+
+
+@pytest.mark.parametrize("which", ["pointsea", "svdformer"])
+def test_shared_partial_fps_model_bitwise(dev, monkeypatch, which):
+    """The models' one shared FPS of the partial cloud (svdformer.shared_partial_fps: the local
+    encoder's local_points FPS, whose first 512 indices are the first SA module's FPS) against the
+    two separate FPS calls of the reference (SVDFormer.py:177 / PointSea.py:241 and
+    model_utils.py:341): a bf16-autocast forward, outputs bitwise equal -- the indices are the same,
+    so is everything computed from them."""
+    import svdformer_pointsea_amd.svdformer as SV
+
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
+    torch.manual_seed(3)
+    if which == "pointsea":
+        model = Model(Config55).cuda().eval()
+        partial, _ = synth_55(2, 9, "cuda")
+        depth = PCViews_Real(TRANS=-Config55.NETWORK.view_distance).get_img(partial)
+    else:
+        from bench import synth_pcn
+        from svdformer_pointsea_amd.render import PCViews
+        model = SV.Model(SV.PCNConfig).cuda().eval()
+        partial, _ = synth_pcn(2, 9, "cuda")
+        depth = PCViews(TRANS=-0.7, RESOLUTION=224).get_img(partial).unsqueeze(1)
+
+    def run(share):
+        monkeypatch.setattr(SV, "_FPS_SHARE", share)
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            return [p.clone() for p in model(partial, depth)]
+
+    run(True)   # first-call algorithm choices out of the way
+    a, b = run(True), run(False)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_seprate_point_cloud_counts_bitwise(dev, monkeypatch):
+    """The crop FPS with per-cloud valid counts (pcops_furthest_point_sampling_counts, rows past the
+    count skipped) returns the input cloud of the plain zero-padded FPS bitwise, crop part included,
+    for random and for fixed crop sizes."""
+    import svdformer_pointsea_amd.data as D
+
+    _, gt = synth_55(4, 13, dev)
+    n = gt.shape[1]
+    for crop in ([n // 4, 3 * n // 4], n // 2, n // 4):
+        out = []
+        for cnt in (True, False):
+            monkeypatch.setattr(D, "_FPS_COUNTS", cnt)
+            out.append(D.seprate_point_cloud(gt, n, crop, generator=torch.Generator(device=dev).manual_seed(9)))
+        (a, ca), (b, cb) = out
+        assert torch.equal(a, b) and torch.equal(ca, cb), crop
