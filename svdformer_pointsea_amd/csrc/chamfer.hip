@@ -317,16 +317,22 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
     __syncthreads();
   }
   // exact re-derivation with the reference expression
+  float bestv[Q];
+  int bkv[Q];
+  bool full[Q], raw[Q];   // raw: ref_scan's result, stored as it is
 #pragma unroll
   for (int i = 0; i < Q; ++i) {
     const int qi = bx * kThreads * Q + i * kThreads + tid;
-    if (qi >= NA) continue;
     float best = INFINITY;
     int bk = 0;
+    full[i] = raw[i] = false;
+    if (qi >= NA) {
+      bestv[i] = best, bkv[i] = bk;
+      continue;
+    }
     if (nanst || !finite3(ax[i], ay[i], az[i])) {
       ref_scan(T, NT, ax[i], ay[i], az[i], best, bk);
-      dist[qi] = best;
-      idx[qi] = bk;
+      bestv[i] = best, bkv[i] = bk, raw[i] = true;
       continue;
     }
     if (!over[i]) {
@@ -358,18 +364,54 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
         }
       }
     }
-    if (over[i] || !(best < INFINITY)) {  // full direct scan (overflow, non-finite data)
-      best = INFINITY;
-      bk = 0;
-      for (int k = 0; k < NT; ++k) {
-        const float d = sqd3(T[3 * k] - ax[i], T[3 * k + 1] - ay[i], T[3 * k + 2] - az[i]);
-        if (d < best) {
-          best = d;
-          bk = k;
+    full[i] = over[i] || !(best < INFINITY);   // slot overflow (near-coincident targets) / overflow risk
+    bestv[i] = best, bkv[i] = bk;
+  }
+  // the full direct scan, for the queries that need it, over the targets staged through LDS by the
+  // whole block (every lane reads the same target: an LDS broadcast).  Degenerate clouds -- a
+  // random-init network's coarse output collapses to a blob -- overflow every query's slots, and the
+  // per-lane scan of global memory it replaced waited out one load latency per target (~0.23 ms per
+  // 2048-target launch in the bench step).
+  bool anyf = false;
+#pragma unroll
+  for (int i = 0; i < Q; ++i) anyf = anyf || full[i];
+  if (__syncthreads_or(anyf)) {
+#pragma unroll
+    for (int i = 0; i < Q; ++i)
+      if (full[i]) bestv[i] = INFINITY, bkv[i] = 0;
+    for (int t0 = 0; t0 < NT; t0 += kTile) {
+      const int cnt = min(kTile, NT - t0);
+      __syncthreads();   // the previous tile is consumed
+      for (int e = tid; e < cnt; e += kThreads) {
+        const float *src = T + (size_t)(t0 + e) * 3;
+        tile[e] = make_float4(src[0], src[1], src[2], 0.f);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        if (!full[i]) continue;
+        float best = bestv[i];
+        int bk = bkv[i];
+        for (int e = 0; e < cnt; ++e) {
+          const float4 p = tile[e];
+          const float d = sqd3(p.x - ax[i], p.y - ay[i], p.z - az[i]);
+          if (d < best) {
+            best = d;
+            bk = t0 + e;
+          }
         }
+        bestv[i] = best, bkv[i] = bk;
       }
     }
-    dist[qi] = best < INFINITY ? best : sqd3(T[3 * bk] - ax[i], T[3 * bk + 1] - ay[i], T[3 * bk + 2] - az[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < Q; ++i) {
+    const int qi = bx * kThreads * Q + i * kThreads + tid;
+    if (qi >= NA) continue;
+    const float best = bestv[i];
+    const int bk = bkv[i];
+    dist[qi] = (raw[i] || best < INFINITY) ? best
+                                           : sqd3(T[3 * bk] - ax[i], T[3 * bk + 1] - ay[i], T[3 * bk + 2] - az[i]);
     idx[qi] = bk;
   }
 }

@@ -21,6 +21,9 @@ for N, M in shapes:
     g = torch.Generator(device="cpu").manual_seed(N + M)
     a = (torch.randn(32, N, 3, generator=g) * 0.45).to(dev)
     b = (torch.randn(32, M, 3, generator=g) * 0.45).to(dev)
+    if os.environ.get("CH_DATA") == "blob":   # xyz1 collapsed to a tiny blob (a random-init coarse output)
+        a = (torch.randn(32, N, 3, generator=g) * 1e-4 + 0.05).to(dev)
+        b = (b / b.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
     if os.environ.get("CH_DATA") == "surface":  # ellipsoid surfaces (completion-like clouds)
         a = (a / a.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
         b = (b / b.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()

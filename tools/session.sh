@@ -1,14 +1,16 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r5d1; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_pointops.py tests/test_gpu_model.py tests/test_gpu_pointsea.py -k "chamfer or model or pointsea or forward or train" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+O=gpurun_out/r5ov; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_pointops.py -k "chamfer or Chamfer" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-export BENCH_AB="PCOPS_CD_DIR1=0;PCOPS_CD_DIR1=1;PCOPS_CD_DIR1=0;PCOPS_CD_DIR1=1"
-bash tools/gpu_run.sh $O bench_ab || exit 1
-for v in 0 1 0 1; do
-  echo "== $v" >> $O/ps.txt
-  PCOPS_CD_DIR1=$v timeout -k 10 300 python bench.py --model pointsea --no-cpu-baseline --no-fp32-leg --no-extra-legs --no-kernel-timing --steps 20 --warmup 3 >> $O/ps.txt 2>> $O/ps.err || exit 1
+SH="2048x2048 512x2048 2048x512 256x256 16384x16384"
+for L in abl6/base/_lib/libpcops.so svdformer_pointsea_amd/_lib/libpcops.so; do
+  for d in blob surface gauss; do
+    PCOPS_LIB_PATH=$L CH_DATA=$d timeout -k 10 60 python tools/chamfer_bench.py 20 $SH >> $O/ab.txt 2>&1 || exit 1
+  done
 done
+grep chamfer $O/ab.txt
+export BENCH_AB="PCOPS_LIB_PATH=abl6/base/_lib/libpcops.so;X=1;PCOPS_LIB_PATH=abl6/base/_lib/libpcops.so;X=1"
+bash tools/gpu_run.sh $O bench_ab || exit 1
 grep -E '^==|ms_per_step' $O/bench_ab.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
-grep -E '^==|ms_per_step' $O/ps.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
