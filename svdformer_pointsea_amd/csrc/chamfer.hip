@@ -276,7 +276,10 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
       over[i] = over[i] || !(eps_t2 + 2.f * anorm[i] * tm < 1e38f);
     }
     const int nsub = (cnt + kSub - 1) / kSub;
-    for (int sb = 0; sb < nsub; ++sb) {
+    bool act = false;   // a query of this lane still screening: an overflowed one takes the full scan anyway
+#pragma unroll
+    for (int i = 0; i < Q; ++i) act = act || !over[i];
+    for (int sb = 0; sb < nsub && act; ++sb) {
       float m[Q];
 #pragma unroll
       for (int i = 0; i < Q; ++i) m[i] = INFINITY;
@@ -392,7 +395,22 @@ __global__ __launch_bounds__(kThreads) void chamfer_screen_kernel(const float *_
         if (!full[i]) continue;
         float best = bestv[i];
         int bk = bkv[i];
-        for (int e = 0; e < cnt; ++e) {
+        // 8 targets' LDS reads issued together, then compared in index order
+        int e = 0;
+        for (; e + 8 <= cnt; e += 8) {
+          float4 p[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p[j] = tile[e + j];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = sqd3(p[j].x - ax[i], p[j].y - ay[i], p[j].z - az[i]);
+            if (d < best) {
+              best = d;
+              bk = t0 + e + j;
+            }
+          }
+        }
+        for (; e < cnt; ++e) {
           const float4 p = tile[e];
           const float d = sqd3(p.x - ax[i], p.y - ay[i], p.z - az[i]);
           if (d < best) {

@@ -24,6 +24,9 @@ for N, M in shapes:
     if os.environ.get("CH_DATA") == "blob":   # xyz1 collapsed to a tiny blob (a random-init coarse output)
         a = (torch.randn(32, N, 3, generator=g) * 1e-4 + 0.05).to(dev)
         b = (b / b.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
+    if os.environ.get("CH_DATA") == "same":   # xyz1: every point the same (a collapsed coarse output)
+        a = torch.full((32, N, 3), 0.05, device=dev)
+        b = (b / b.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
     if os.environ.get("CH_DATA") == "surface":  # ellipsoid surfaces (completion-like clouds)
         a = (a / a.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
         b = (b / b.norm(dim=-1, keepdim=True) * torch.tensor([0.5, 0.3, 0.15], device=dev)).contiguous()
