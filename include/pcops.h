@@ -309,15 +309,16 @@ int pcops_layernorm_bwd(const float *dy32, const void *dy16, const void *a, int 
                         const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
                         void *dx16, float *dgamma, float *dbeta, void *workspace, unsigned long long workspace_bytes,
                         pcops_stream_t stream);
-/* pcops_layernorm_bwd_colsum: pcops_layernorm_bwd plus dsum[c] = sum_r dx[r][c] (C fp32):
+/* pcops_layernorm_bwd_colsum: pcops_layernorm_bwd plus dsum[c] = sum_r dx[r][c] (C values):
  *   the bias gradient of the Linear / 1x1 conv whose output is a LayerNorm input (a or b),
- *   summed over dx as stored -- dx16's bf16 values (dsum_src = 1) or dx32's (dsum_src = 0) --
- *   in the same launch (replaces that layer's separate pcops_colsum over dx).
+ *   summed over dx as stored -- dx16's bf16 values (dsum_src bit 0 = 1) or dx32's (bit 0 = 0) --
+ *   in the same launch (replaces that layer's separate pcops_colsum over dx).  dsum_src bit 1:
+ *   dsum stored bf16 (rounded once from the fp32 sum: the consuming bias's dtype), else fp32.
  *   workspace: pcops_layernorm_bwd_colsum_workspace_bytes. */
 unsigned long long pcops_layernorm_bwd_colsum_workspace_bytes(int rows, int C);
 int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b,
                                int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
-                               float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
+                               float *dx32, void *dx16, float *dgamma, float *dbeta, void *dsum, int dsum_src,
                                void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_adam_flat: torch's Adam (adamw = 0; weight decay added to the gradient) or AdamW (adamw = 1;
  *   decoupled decay) over n fp32 master weights `param` with its exp_avg / exp_avg_sq state
@@ -348,15 +349,16 @@ int pcops_blend_bwd(const void *g, int g_dtype, const void *score, int score_dty
  *   Replaces the autograd cast in front of nn.LayerNorm's backward (models/model_utils.py:600-617). */
 int pcops_layernorm_bwd_bf16g(const void *dy_a, const void *dy16, const void *a, int a_dtype, const void *b,
                               int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
-                              float *dx32, void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src,
+                              float *dx32, void *dx16, float *dgamma, float *dbeta, void *dsum, int dsum_src,
                               void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_gelu_bwd_colsum: du = dy * GELU'(u) (exact erf GELU, torch's GeluBackward expression in
  *   fp32) over a row-major (rows, C) matrix, dy / u / du all `dtype` (0 fp32, 1 bf16), C % 8 == 0;
- *   when dsum != NULL also dsum[c] = sum_r du[r][c] over du as stored (C fp32): the bias gradient
- *   of the Linear whose output u the GELU consumed (the blocks' linear11, models/model_utils.py:612),
- *   in place of a separate pcops_colsum.  workspace: pcops_colsum_workspace_bytes(rows, C) when dsum. */
-int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, long long rows, int C, void *du, float *dsum,
-                          void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+ *   when dsum != NULL also dsum[c] = sum_r du[r][c] over du as stored (C values, fp32 accumulation,
+ *   stored as dsum_dtype: the consuming bias's dtype): the bias gradient of the Linear whose output u
+ *   the GELU consumed (the blocks' linear11, models/model_utils.py:612), in place of a separate
+ *   pcops_colsum.  workspace: pcops_colsum_workspace_bytes(rows, C) when dsum. */
+int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, long long rows, int C, void *du, void *dsum,
+                          int dsum_dtype, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_colsum: out[c] = sum_r g[r][c] over a row-major (rows, C) matrix, C % 8 == 0,
  *   fp32 accumulation in a fixed order (deterministic); g / out dtype codes 0 fp32, 1 bf16.
  *   Replaces the bias-gradient reduction autograd runs for nn.Linear / 1x1 nn.Conv*d biases

@@ -69,7 +69,7 @@ _SIGS = {
     "pcops_edge_group_grad": (I, [P, I, P, I, I, I, I, P, P]),
     "pcops_max_k": (I, [P, I, LL, I, I, P, P, P]),
     "pcops_max_k_grad": (I, [P, I, P, LL, I, I, P, P]),
-    "pcops_gelu_bwd_colsum": (I, [P, P, I, LL, I, P, P, P, ULL, P]),
+    "pcops_gelu_bwd_colsum": (I, [P, P, I, LL, I, P, P, I, P, ULL, P]),
     "pcops_layernorm_fwd": (I, [P, I, P, I, P, P, F, I, I, P, P, P, P, P]),
     "pcops_layernorm_bwd_workspace_bytes": (ULL, [I, I]),
     "pcops_layernorm_bwd": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, ULL, P]),

@@ -146,6 +146,14 @@ class _Linear(Function):
 _PRESUM = "_pcops_bias_colsum"   # attribute a gradient tensor carries when its column sum is known
 
 
+def _sum_dtype(t):
+    """The dtype the fused bias sum of t's gradient is stored in: the bias dtype of the _Linear that
+    produced t (its backward then takes the sum without a cast launch), fp32 otherwise."""
+    fn = t.grad_fn if t is not None else None
+    bdt = getattr(fn, "b_dtype", None) if fn is not None and type(fn).__name__ == "_LinearBackward" else None
+    return bdt if bdt in (torch.float32, torch.bfloat16) and _SUM_IN_BIAS_DTYPE else torch.float32
+
+
 def _attach_sum(g, dsum):
     """Hand the column sum of gradient `g` (computed by the launch that wrote g)
     to the _Linear backward that consumes g, as (sum, producing stream)."""
@@ -512,6 +520,7 @@ class _LayerNorm(Function):
         ctx.save_for_backward(a, b, w, mean, rstd)
         ctx.wdt = weight.dtype
         ctx.sum_of = sum_of
+        ctx.sum_dt = _sum_dtype((a, b)[sum_of]) if sum_of is not None else torch.float32
         if y16 is None:
             return y32
         return y32, y16
@@ -533,24 +542,26 @@ class _LayerNorm(Function):
         db = torch.empty_like(dw)
         src = None if ctx.sum_of is None else (a, b)[ctx.sum_of]
         need = (ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        sflag = 2 if ctx.sum_dt == torch.bfloat16 else 0   # dsum_src bit 1: the sum stored bf16
         if ga16 is not None:   # both upstream gradients bf16: widened inside the launch
-            dsum = torch.empty_like(dw) if (src is not None and need[ctx.sum_of]) else None
+            dsum = (torch.empty(C, dtype=ctx.sum_dt, device=a.device) if (src is not None and need[ctx.sum_of])
+                    else None)
             wsb = (lib().pcops_layernorm_bwd_colsum_workspace_bytes(rows, C) if dsum is not None
                    else lib().pcops_layernorm_bwd_workspace_bytes(rows, C))
             ws = _lib.Workspace.get(a.device, wsb)
             with torch.cuda.device(a.device):
                 call("layernorm_bwd", lib().pcops_layernorm_bwd_bf16g, ptr(ga16), ptr(g16), ptr(a), _dt(a), ptr(b),
                      0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16),
-                     ptr(dw), ptr(db), ptr(dsum), _DT[src.dtype] if dsum is not None else 0, ptr(ws), wsb,
+                     ptr(dw), ptr(db), ptr(dsum), (_DT[src.dtype] | sflag) if dsum is not None else 0, ptr(ws), wsb,
                      stream_of(a))
         elif src is not None and need[ctx.sum_of]:
-            dsum = torch.empty_like(dw)
+            dsum = torch.empty(C, dtype=ctx.sum_dt, device=a.device)
             wsb = lib().pcops_layernorm_bwd_colsum_workspace_bytes(rows, C)
             ws = _lib.Workspace.get(a.device, wsb)
             with torch.cuda.device(a.device):
                 call("layernorm_bwd", lib().pcops_layernorm_bwd_colsum, ptr(g32), ptr(g16), ptr(a), _dt(a), ptr(b),
                      0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16),
-                     ptr(dw), ptr(db), ptr(dsum), _DT[src.dtype], ptr(ws), wsb, stream_of(a))
+                     ptr(dw), ptr(db), ptr(dsum), _DT[src.dtype] | sflag, ptr(ws), wsb, stream_of(a))
         else:
             dsum = None
             wsb = lib().pcops_layernorm_bwd_workspace_bytes(rows, C)
@@ -604,6 +615,7 @@ class _Gelu(Function):
     def forward(ctx, u, want_sum):
         ctx.save_for_backward(u)
         ctx.want_sum = want_sum
+        ctx.sum_dt = _sum_dtype(u) if want_sum else torch.float32
         return F.gelu(u)   # torch's vectorised kernel runs this 1:1 stream at ~4.1 TB/s; a libpcops
         # kernel (4 x 8 elements in flight per thread) measured the same step time (r4 A/B)
 
@@ -614,12 +626,12 @@ class _Gelu(Function):
         C = u.shape[-1]
         rows = u.numel() // C
         du = torch.empty_like(u)
-        dsum = torch.empty(C, dtype=torch.float32, device=u.device) if ctx.want_sum else None
+        dsum = torch.empty(C, dtype=ctx.sum_dt, device=u.device) if ctx.want_sum else None
         wsb = lib().pcops_colsum_workspace_bytes(rows, C) if ctx.want_sum else 0
         ws = _lib.Workspace.get(u.device, wsb) if ctx.want_sum else None
         with torch.cuda.device(u.device):
             call("gelu_bwd", lib().pcops_gelu_bwd_colsum, ptr(g), ptr(u), _dt(u), rows, C, ptr(du), ptr(dsum),
-                 ptr(ws), wsb, stream_of(u))
+                 _DT[ctx.sum_dt], ptr(ws), wsb, stream_of(u))
         if dsum is not None:
             _attach_sum(du, dsum)
         return du, None
@@ -842,6 +854,8 @@ _WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switc
 _WGRAD_SMALL = os.environ.get("PCOPS_WGRAD_SMALL", "1") != "0"    # A/B switch: more split-K slices for small weights
 _WGRAD_SMALL_LOG2 = int(os.environ.get("PCOPS_WGRAD_SMALL_LOG2", "20"))  # partial elements aimed at (log2)
 _WGRAD_MINK = int(os.environ.get("PCOPS_WGRAD_MINK", "2048"))   # tokens per split-K slice at least (S <= 16)
+# PCOPS_SUM_BIAS_DTYPE=0: fused bias sums stay fp32 and the Linear backward casts them (A/B runs)
+_SUM_IN_BIAS_DTYPE = os.environ.get("PCOPS_SUM_BIAS_DTYPE", "1") != "0"
 _PCOPS_GELU = os.environ.get("PCOPS_GELU", "1") != "0"               # A/B switch: fused-backward GELU
 _FUSED_SIDE = os.environ.get("PCOPS_FUSED_SIDE", "0") == "1"          # diagnostic: fused sums in side-stream blocks too
 # linear11's bias sum inside the GELU backward (A/B switch); the sum reaches the

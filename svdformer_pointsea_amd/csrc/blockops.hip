@@ -559,7 +559,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const void *__restr
 __global__ __launch_bounds__(1024) void colsum_final_kernel(const float *__restrict__ part, int chunks, int C,
                                                             void *__restrict__ out, int odt, int split,
                                                             void *__restrict__ out2, int split2,
-                                                            void *__restrict__ out3) {
+                                                            void *__restrict__ out3, int odt3) {
   __shared__ float red[32][33];
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int col = blockIdx.x * 32 + cl;
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float *__restr
     else if (col < split2)
       st(out2, odt, col - split, tot);
     else
-      st(out3, odt, col - split2, tot);
+      st(out3, odt3, col - split2, tot);
   }
 }
 
@@ -590,7 +590,7 @@ template <int CW>
 __global__ __launch_bounds__(1024) void colsum_final_cw_kernel(const float *__restrict__ part, int chunks, int C,
                                                                void *__restrict__ out, int odt, int split,
                                                                void *__restrict__ out2, int split2,
-                                                               void *__restrict__ out3) {
+                                                               void *__restrict__ out3, int odt3) {
   constexpr int G = 1024 / CW, U = 8;
   __shared__ float red[G][CW + 1];
   const int cl = threadIdx.x % CW, grp = threadIdx.x / CW;
@@ -618,22 +618,24 @@ __global__ __launch_bounds__(1024) void colsum_final_cw_kernel(const float *__re
     else if (col < split2)
       st(out2, odt, col - split, tot);
     else
-      st(out3, odt, col - split2, tot);
+      st(out3, odt3, col - split2, tot);
   }
 }
 
+// out3 (the fused bias sum) in its own dtype odt3: the consuming Linear's bias dtype, so no cast follows
 void launch_colsum_final(const float *part, int chunks, int C, void *out, int odt, int split, void *out2,
-                         int split2, void *out3, hipStream_t s) {
+                         int split2, void *out3, hipStream_t s, int odt3 = -1) {
+  if (odt3 < 0) odt3 = odt;
   static const int cw = [] {
     const char *e = getenv("PCOPS_COLSUM_FINAL_CW");
     return e ? atoi(e) : 32;
   }();
   if (cw == 16)
     hipLaunchKernelGGL(colsum_final_cw_kernel<16>, dim3((C + 15) / 16), dim3(1024), 0, s, part, chunks, C, out, odt,
-                       split, out2, split2, out3);
+                       split, out2, split2, out3, odt3);
   else
     hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 31) / 32), dim3(1024), 0, s, part, chunks, C, out, odt, split,
-                       out2, split2, out3);
+                       out2, split2, out3, odt3);
 }
 
 // GELU backward (exact erf form, torch's GeluBackward expression in fp32) fused
@@ -1026,18 +1028,21 @@ extern "C" unsigned long long pcops_layernorm_bwd_workspace_bytes(int rows, int 
 namespace {
 int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a_dtype, const void *b, int b_dtype,
                        const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
-                       void *dx16, float *dgamma, float *dbeta, float *dsum, int dsum_src, void *workspace,
+                       void *dx16, float *dgamma, float *dbeta, void *dsum, int dsum_src, void *workspace,
                        unsigned long long workspace_bytes, unsigned long long need, hipStream_t s,
                        bool dy32_bf16 = false) {
   if (rows < 0 || C <= 0) return PCOPS_ERR_INVALID;
   if (C > 512 * kMaxCh || C % 8) return PCOPS_ERR_UNSUPPORTED;
   if (!dgamma || !dbeta) return PCOPS_ERR_INVALID;
-  if (dsum && ((dsum_src == 1 && !dx16) || (dsum_src == 0 && !dx32) || (dsum_src != 0 && dsum_src != 1)))
+  if (dsum_src & ~3) return PCOPS_ERR_INVALID;
+  const int dsum_dt = (dsum_src >> 1) & 1;   // bit 1: dsum stored bf16 (the consuming bias's dtype)
+  dsum_src &= 1;
+  if (dsum && ((dsum_src == 1 && !dx16) || (dsum_src == 0 && !dx32)))
     return PCOPS_ERR_INVALID;
   if (rows == 0) {
     if (pc_memset_async(dgamma, 0, sizeof(float) * C, s) != hipSuccess ||
         pc_memset_async(dbeta, 0, sizeof(float) * C, s) != hipSuccess ||
-        (dsum && pc_memset_async(dsum, 0, sizeof(float) * C, s) != hipSuccess))
+        (dsum && pc_memset_async(dsum, 0, (dsum_dt ? 2 : 4) * (size_t)C, s) != hipSuccess))
       return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
@@ -1066,7 +1071,7 @@ int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a
   ln_dispatch<LnBwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p,
                       (dy32 ? 1 : 0) | (dy16 ? 2 : 0) | (dy32_bf16 ? 4 : 0), blocks, ln_bwd_rpw(rows));
   const int np = dsum ? 3 : 2;
-  launch_colsum_final(part, blocks, np * C, (void *)dgamma, 0, C, (void *)dbeta, 2 * C, (void *)dsum, s);
+  launch_colsum_final(part, blocks, np * C, (void *)dgamma, 0, C, (void *)dbeta, 2 * C, dsum, s, dsum_dt);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
@@ -1089,7 +1094,7 @@ extern "C" unsigned long long pcops_layernorm_bwd_colsum_workspace_bytes(int row
 extern "C" int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, const void *a, int a_dtype,
                                           const void *b, int b_dtype, const float *gamma, const float *mean,
                                           const float *rstd, int rows, int C, float *dx32, void *dx16, float *dgamma,
-                                          float *dbeta, float *dsum, int dsum_src, void *workspace,
+                                          float *dbeta, void *dsum, int dsum_src, void *workspace,
                                           unsigned long long workspace_bytes, pcops_stream_t stream) {
   if (!dsum) return PCOPS_ERR_INVALID;
   return layernorm_bwd_impl(dy32, dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, dx16, dgamma, dbeta,
@@ -1100,7 +1105,7 @@ extern "C" int pcops_layernorm_bwd_colsum(const float *dy32, const void *dy16, c
 extern "C" int pcops_layernorm_bwd_bf16g(const void *dy_a, const void *dy16, const void *a, int a_dtype,
                                          const void *b, int b_dtype, const float *gamma, const float *mean,
                                          const float *rstd, int rows, int C, float *dx32, void *dx16, float *dgamma,
-                                         float *dbeta, float *dsum, int dsum_src, void *workspace,
+                                         float *dbeta, void *dsum, int dsum_src, void *workspace,
                                          unsigned long long workspace_bytes, pcops_stream_t stream) {
   if (!dy_a || !dy16) return PCOPS_ERR_INVALID;
   return layernorm_bwd_impl((const float *)dy_a, dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, dx16,
@@ -1119,13 +1124,13 @@ extern "C" unsigned long long pcops_colsum_workspace_bytes(long long rows, int C
 }
 
 extern "C" int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, long long rows, int C, void *du,
-                                     float *dsum, void *workspace, unsigned long long workspace_bytes,
+                                     void *dsum, int dsum_dtype, void *workspace, unsigned long long workspace_bytes,
                                      pcops_stream_t stream) {
-  if (rows < 0 || C <= 0 || !dt_ok(dtype)) return PCOPS_ERR_INVALID;
+  if (rows < 0 || C <= 0 || !dt_ok(dtype) || (dsum && !dt_ok(dsum_dtype))) return PCOPS_ERR_INVALID;
   if (C % 8) return PCOPS_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   if (rows == 0) {
-    if (dsum && pc_memset_async(dsum, 0, sizeof(float) * C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
+    if (dsum && pc_memset_async(dsum, 0, (dsum_dtype == 0 ? 4 : 2) * (size_t)C, s) != hipSuccess) return PCOPS_ERR_LAUNCH;
     return PCOPS_OK;
   }
   if (!dy || !u || !du) return PCOPS_ERR_INVALID;
@@ -1141,7 +1146,7 @@ extern "C" int pcops_gelu_bwd_colsum(const void *dy, const void *u, int dtype, l
       hipLaunchKernelGGL((gelu_bwd_partial_kernel<0, true>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc, part);
     else
       hipLaunchKernelGGL((gelu_bwd_partial_kernel<1, true>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc, part);
-    launch_colsum_final(part, chunks, C, (void *)dsum, 0, C, nullptr, C, nullptr, s);
+    launch_colsum_final(part, chunks, C, dsum, dsum_dtype, C, nullptr, C, nullptr, s);
   } else {
     if (dtype == 0)
       hipLaunchKernelGGL((gelu_bwd_partial_kernel<0, false>), grid, dim3(256), 0, s, dy, u, du, rows, C, V, rpc,

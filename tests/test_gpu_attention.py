@@ -681,6 +681,37 @@ def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
         torch.testing.assert_close(g_fus[n], g_ref[n], **tol, msg=n)
 
 
+def test_fused_bias_sum_in_bias_dtype_bitwise(dev, monkeypatch):
+    """With bf16 biases (bench.py's FlatParams shadows) the fused bias sums of the LayerNorm and GELU
+    backwards are stored in bf16 by the summing launch itself (round 5), so the Linear backward takes
+    them without a cast launch: every gradient bitwise equal to the fp32-sum-then-cast path."""
+    import copy
+
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(1)
+    blk = A.self_attention(64, 128, nhead=2).to(dev)
+    for n, p in blk.named_parameters():
+        if n.endswith("bias") and "norm" not in n and "in_proj" not in n:
+            p.data = p.data.to(torch.bfloat16)
+    x = torch.randn(4, 64, 2048, device=dev)            # 8192 tokens: the _Linear path
+    monkeypatch.setattr(A, "_GELU_SUM", True)
+    monkeypatch.setattr(A, "_FUSED_BIAS_SUM", True)
+
+    def run(flag):
+        monkeypatch.setattr(A, "_SUM_IN_BIAS_DTYPE", flag)
+        m = copy.deepcopy(blk)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x)
+        (y.float() ** 2).mean().backward()
+        return {n: p.grad.clone() for n, p in m.named_parameters()}
+
+    a, b = run(False), run(True)
+    assert any(g.dtype == torch.bfloat16 for g in b.values())
+    for n in a:
+        assert a[n].dtype == b[n].dtype and torch.equal(a[n], b[n]), n
+
+
 @pytest.mark.parametrize("S", [16, 32, 64, 128, 256, 512])
 @pytest.mark.parametrize("N", [192, 2048, 8192, 16384, 32768, 65536, 131072, 1 << 20])
 def test_sum_rows_matches_float64(dev, S, N):
