@@ -425,6 +425,12 @@ int pcops_batchnorm_bwd(const void *dy, const void *y, const void *x, int dtype,
  *   fp32 accumulation, block partials summed in a fixed order.
  *   workspace: pcops_conv3x3_wgrad_workspace_bytes(C). */
 int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int W, int C, void *y, pcops_stream_t stream);
+/* pcops_conv3x3_fwd_res: pcops_conv3x3_fwd plus a residual: y = bf16(float(bf16(conv(x, w))) + float(res)),
+ *   res bf16 in y's layout.  The input gradient of a ResNet BasicBlock's first conv (the dgrad form of this
+ *   conv) fused with the gradient the block input also gets through the identity branch -- autograd's
+ *   bf16 accumulation of the two (models/resnet.py:56-70: `out += identity`), without its separate add pass. */
+int pcops_conv3x3_fwd_res(const void *x, const void *w, int N, int H, int W, int C, const void *res, void *y,
+                          pcops_stream_t stream);
 unsigned long long pcops_conv3x3_wgrad_workspace_bytes(int C);
 int pcops_conv3x3_wgrad(const void *x, const void *dy, int N, int H, int W, int C, void *dw, int dw_dtype,
                         int dw_ohwi, void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);

@@ -89,6 +89,7 @@ _SIGS = {
     "pcops_batchnorm_fwd": (I, [P, I, P, I, LL, I, P, P, P, P, F, F, I, I, F, P, P, P, P, ULL, P, P]),
     "pcops_batchnorm_bwd": (I, [P, P, P, I, LL, I, P, P, P, I, I, F, P, P, P, P, P, ULL, P]),
     "pcops_conv3x3_fwd": (I, [P, P, I, I, I, I, P, P]),
+    "pcops_conv3x3_fwd_res": (I, [P, P, I, I, I, I, P, P, P]),
     "pcops_conv3x3_wgrad_workspace_bytes": (ULL, [I]),
     "pcops_conv3x3_wgrad": (I, [P, P, I, I, I, I, P, I, I, P, ULL, P]),
     "pcops_conv3x3_c1_fwd": (I, [P, P, I, I, I, P, P]),

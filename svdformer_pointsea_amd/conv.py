@@ -47,14 +47,56 @@ class _Conv3x3(torch.autograd.Function):
                 gx = torch.empty_like(x)
                 call("conv3x3_dgrad", lib().pcops_conv3x3_fwd, ptr(gy), ptr(wt), N, H, W, C, ptr(gx), stream_of(x))
             if ctx.needs_input_grad[1]:
-                gw = torch.empty_like(w)   # w's dtype and memory order (OIHW or channels_last OHWI)
-                ohwi = int(w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous())
-                if not (ohwi or w.is_contiguous()):
-                    gw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
-                nbytes = lib().pcops_conv3x3_wgrad_workspace_bytes(C)
-                ws = Workspace.get(x.device, nbytes)
-                call("conv3x3_wgrad", lib().pcops_conv3x3_wgrad, ptr(x), ptr(gy), N, H, W, C, ptr(gw),
-                     0 if w.dtype == torch.float32 else 1, ohwi, ptr(ws), nbytes, stream_of(x))
+                gw = _Conv3x3._wgrad(x, w, gy)
+        return gx, gw
+
+    @staticmethod
+    def _wgrad(x, w, gy):
+        N, C, H, W = x.shape
+        gw = torch.empty_like(w)   # w's dtype and memory order (OIHW or channels_last OHWI)
+        ohwi = int(w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous())
+        if not (ohwi or w.is_contiguous()):
+            gw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
+        nbytes = lib().pcops_conv3x3_wgrad_workspace_bytes(C)
+        ws = Workspace.get(x.device, nbytes)
+        call("conv3x3_wgrad", lib().pcops_conv3x3_wgrad, ptr(x), ptr(gy), N, H, W, C, ptr(gw),
+             0 if w.dtype == torch.float32 else 1, ohwi, ptr(ws), nbytes, stream_of(x))
+        return gw
+
+
+class _Conv3x3Skip(torch.autograd.Function):
+    """(conv(x), x) for a ResNet BasicBlock whose input also feeds its identity branch: the two gradients
+    x receives (the first conv's input gradient and the identity's) are summed inside the dgrad launch
+    (pcops_conv3x3_fwd_res) as autograd's bf16 accumulation would sum them, instead of a separate add
+    pass over the block input (models/resnet.py:56-70 `out += identity`)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.set_materialize_grads(False)
+        y = _Conv3x3.forward(ctx, x, w)
+        return y, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gskip):
+        x, w = ctx.saved_tensors
+        N, C, H, W = x.shape
+        gx = gw = None
+        if gy is None:
+            return (None if gskip is None else gskip.to(x.dtype)), None
+        gy = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        with torch.cuda.device(x.device):
+            if ctx.needs_input_grad[0]:
+                wt = w.to(torch.bfloat16).flip(2, 3).permute(1, 2, 3, 0).contiguous()
+                gx = torch.empty_like(x)
+                if gskip is None:
+                    call("conv3x3_dgrad", lib().pcops_conv3x3_fwd, ptr(gy), ptr(wt), N, H, W, C, ptr(gx),
+                         stream_of(x))
+                else:
+                    r = gskip.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                    call("conv3x3_dgrad_res", lib().pcops_conv3x3_fwd_res, ptr(gy), ptr(wt), N, H, W, C, ptr(r),
+                         ptr(gx), stream_of(x))
+            if ctx.needs_input_grad[1]:
+                gw = _Conv3x3._wgrad(x, w, gy)
         return gx, gw
 
 
@@ -107,6 +149,19 @@ def eligible(x, conv):
             and C in _CHANNELS and conv.in_channels == C and conv.out_channels == C
             and conv.weight.dtype in (torch.float32, torch.bfloat16)
             and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+
+
+# PCOPS_CONV_SKIP=0: the BasicBlock's identity gradient added by autograd (A/B runs)
+SKIP_FUSED = os.environ.get("PCOPS_CONV_SKIP", "1") != "0"
+
+
+def conv3x3_skip(x, conv):
+    """(conv(x), identity of x) for a BasicBlock without downsample: on libpcops the identity's
+    gradient is summed into the conv's input gradient inside the dgrad launch (_Conv3x3Skip)."""
+    w = conv.weight
+    if SKIP_FUSED and eligible(x, conv) and w.dtype in (torch.float32, torch.bfloat16) and torch.is_grad_enabled():
+        return _Conv3x3Skip.apply(x, w)
+    return conv3x3(x, conv), x
 
 
 def conv3x3(x, conv, weight=None):

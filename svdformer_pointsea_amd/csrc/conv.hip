@@ -75,10 +75,13 @@ __device__ __forceinline__ long long xcd_tile(long long b, long long tiles) {
 }
 
 // ---------------------------------------------------------------- forward / dgrad
+// res != nullptr: y = bf16(float(bf16(conv)) + float(res)) -- the input gradient of a BasicBlock's
+// first conv plus the gradient its input also receives through the block's identity branch, added
+// exactly as autograd's bf16 accumulation of the two would (both terms rounded to bf16 first)
 template <int CI, int CO, int TW>
 __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(const __bf16 *__restrict__ x,
                                                           const __bf16 *__restrict__ w, __bf16 *__restrict__ y,
-                                                          int H, int W, int N) {
+                                                          int H, int W, int N, const __bf16 *__restrict__ res) {
   constexpr int KC = (9 * CI + 31) / 32;  // K chunks of 32 over (tap, ci); the tail has zero weights
   constexpr int MT = CO / 16;
   constexpr int LW = TW + 2;
@@ -122,12 +125,20 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(const __bf16 *__restri
     }
     const int ow = w0 + pc;
     if (orow < H && ow < W) {
-      __bf16 *yp = y + (((long long)n * H + orow) * W + ow) * CO + 4 * g;
+      const long long e0 = (((long long)n * H + orow) * W + ow) * CO + 4 * g;
+      __bf16 *yp = y + e0;
+      bf16x4 rv[MT];
+      if (res)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) rv[mt] = *reinterpret_cast<const bf16x4 *>(res + e0 + 16 * mt);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[mt][r];
+        if (res)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (__bf16)((float)o[r] + (float)rv[mt][r]);
         *reinterpret_cast<bf16x4 *>(yp + 16 * mt) = o;
       }
     }
@@ -487,12 +498,14 @@ __global__ __launch_bounds__(256) void conv3x3_c1_wgrad_kernel(const float *__re
 
 }  // namespace
 
-extern "C" int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int W, int C, void *y,
-                                 pcops_stream_t stream) {
+namespace {
+int conv3x3_fwd_impl(const void *x, const void *w, int N, int H, int W, int C, const void *res, void *y,
+                     pcops_stream_t stream) {
   if (N < 0 || H < 0 || W < 0) return PCOPS_ERR_INVALID;
   if (N == 0 || H == 0 || W == 0) return PCOPS_OK;
   if (!conv_ok(N, H, W, C)) return PCOPS_ERR_UNSUPPORTED;
   if (!x || !w || !y) return PCOPS_ERR_INVALID;
+  const __bf16 *rp = (const __bf16 *)res;
   hipStream_t s = (hipStream_t)stream;
   // 112-column tiles where they divide W exactly (the 224 / 112 images): no masked N-tiles
   const bool wide = W % 112 == 0;
@@ -502,14 +515,26 @@ extern "C" int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int
   const __bf16 *xp = (const __bf16 *)x, *wp = (const __bf16 *)w;
   __bf16 *yp = (__bf16 *)y;
   if (C == 16) {
-    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
-    else hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
+    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N, rp);
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<16, 16, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N, rp);
   } else {
-    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
-    else hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N);
+    if (wide) hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 112>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N, rp);
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<32, 32, 64>), grid, dim3(256), 0, s, xp, wp, yp, H, W, N, rp);
   }
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
+}
+}  // namespace
+
+extern "C" int pcops_conv3x3_fwd(const void *x, const void *w, int N, int H, int W, int C, void *y,
+                                 pcops_stream_t stream) {
+  return conv3x3_fwd_impl(x, w, N, H, W, C, nullptr, y, stream);
+}
+
+extern "C" int pcops_conv3x3_fwd_res(const void *x, const void *w, int N, int H, int W, int C, const void *res,
+                                     void *y, pcops_stream_t stream) {
+  if (!res) return PCOPS_ERR_INVALID;
+  return conv3x3_fwd_impl(x, w, N, H, W, C, res, y, stream);
 }
 
 extern "C" unsigned long long pcops_conv3x3_wgrad_workspace_bytes(int C) {

@@ -26,7 +26,7 @@ from .model_utils import (SharedFPS, edge_features, fps_subsample, group_local, 
                           sample_and_group_knn_cl)
 from ._lib import fork
 from .batchnorm import ACT_RELU, bn_act, run_sequential
-from .conv import conv3x3
+from .conv import conv3x3, conv3x3_skip
 from .pointnet2_utils import furthest_point_sample, gather_operation
 
 
@@ -383,8 +383,13 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         # bn + (residual) + relu fused on libpcops (batchnorm.bn_act; torch's modules when not fusable)
         # 3x3 stride-1 convs at C = 16 / 32 on libpcops MFMA kernels (conv.conv3x3; MIOpen otherwise)
-        identity = x if self.downsample is None else run_sequential(self.downsample, x)
-        out = bn_act(conv3x3(x, self.conv1), self.bn1, ACT_RELU)
+        if self.downsample is None:
+            # x feeds conv1 and the identity: its two gradients are summed inside conv1's dgrad launch
+            y1, identity = conv3x3_skip(x, self.conv1)
+        else:
+            identity = run_sequential(self.downsample, x)
+            y1 = conv3x3(x, self.conv1)
+        out = bn_act(y1, self.bn1, ACT_RELU)
         return bn_act(conv3x3(out, self.conv2), self.bn2, ACT_RELU, residual=identity)
 
 

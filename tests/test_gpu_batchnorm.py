@@ -305,3 +305,34 @@ def test_bn_fused_final_graph_replays(dev):
         got = [y, xg.grad, bn.weight.grad, bn.bias.grad]
         for u, v in zip(ref, got):
             assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("C,HW", [(16, 56), (32, 28), (16, 224)])
+def test_basic_block_skip_fused_bitwise(dev, monkeypatch, C, HW):
+    """A stride-1 BasicBlock's input gradient with the identity's share summed inside conv1's dgrad
+    launch (conv._Conv3x3Skip -> pcops_conv3x3_fwd_res) against autograd's separate bf16 add: the
+    output, the input gradient and every parameter gradient bitwise equal, bf16 autocast."""
+    import svdformer_pointsea_amd.conv as CV
+
+    torch.manual_seed(C + HW)
+    blk = S.BasicBlock(C, C).to(dev).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        for m in blk.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(4, C, HW, HW, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(4, C, HW, HW, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(fused):
+        monkeypatch.setattr(CV, "SKIP_FUSED", fused)
+        m = copy.deepcopy(blk)
+        xg = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(xg)
+        y.backward(dy)
+        return [y.detach(), xg.grad] + [p.grad for p in m.parameters()]
+
+    a, b = run(False), run(True)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), i
