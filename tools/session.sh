@@ -1,9 +1,4 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r5sk; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_batchnorm.py tests/test_gpu_conv.py tests/test_gpu_model.py tests/test_gpu_pointsea.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -2 $O/pytest.log
-export BENCH_AB="PCOPS_CONV_SKIP=0;PCOPS_CONV_SKIP=1;PCOPS_CONV_SKIP=0;PCOPS_CONV_SKIP=1"
-bash tools/gpu_run.sh $O bench_ab || exit 1
-grep -E '^==|ms_per_step' $O/bench_ab.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
+bash tools/gpu_run.sh gpurun_out/r5f2 tests smoke bench trace
