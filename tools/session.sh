@@ -1,14 +1,13 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
 # stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r5cf; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/r5nd; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_attention.py tests/test_gpu_model.py tests/test_gpu_train_step.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-export BENCH_AB="PCOPS_COLSUM_FUSED=0;PCOPS_COLSUM_FUSED=1;PCOPS_COLSUM_FUSED=0;PCOPS_COLSUM_FUSED=1"
+OLD=PCOPS_LIB_PATH=abl6/libpcops_old.so
+export ATTN_AB="X=new;$OLD;X=new;$OLD" ATTN_SHAPES="0 1 3"
+bash tools/gpu_run.sh $O attn_ab || exit 1
+grep -E "^==|bwd|dkv" $O/attn_ab.txt | head -60
+export BENCH_AB="X=new;$OLD;X=new;$OLD"
 bash tools/gpu_run.sh $O bench_ab || exit 1
 grep -E '^==|ms_per_step' $O/bench_ab.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
-for v in 0 1 0 1; do
-  echo "== $v" >> $O/ps.txt
-  PCOPS_COLSUM_FUSED=$v timeout -k 10 300 python bench.py --model pointsea --no-cpu-baseline --no-fp32-leg --no-extra-legs --no-kernel-timing --steps 20 --warmup 3 >> $O/ps.txt 2>> $O/ps.err || exit 1
-done
-grep -E '^==|ms_per_step' $O/ps.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
