@@ -72,8 +72,19 @@ __device__ __forceinline__ float act_bwd(float dy, float y, float slope) {
   return dy;
 }
 
-constexpr int kBnMaxChunks = 256;  // partial rows; one 16-wave block per chunk
-constexpr int kBnWaves = 16;
+// A/B builds override these with -D (csrc/Makefile EXTRA)
+#ifndef PCOPS_BN_CHUNKS
+#define PCOPS_BN_CHUNKS 256
+#endif
+#ifndef PCOPS_BN_WAVES
+#define PCOPS_BN_WAVES 16
+#endif
+#ifndef PCOPS_BN_UNROLL
+#define PCOPS_BN_UNROLL 4
+#endif
+constexpr int kBnMaxChunks = PCOPS_BN_CHUNKS;  // partial rows; one kBnWaves-wave block per chunk
+constexpr int kBnWaves = PCOPS_BN_WAVES;
+constexpr int kBnUnroll = PCOPS_BN_UNROLL;     // rows whose loads issue together per lane
 
 int bn_v(int C) {  // vector columns per wave: largest power of two <= 64 dividing C / 8
   const int nv = C / 8;
@@ -82,9 +93,16 @@ int bn_v(int C) {  // vector columns per wave: largest power of two <= 64 dividi
   return V;
 }
 
+// chunks per launch: kBnMaxChunks, half that below 2^25 elements (the ResNet's layer3 / layer4
+// activations: fewer partial rows for the final; profiles/r5_bn_variants.txt)
+int bn_max_chunks(long long rows, int C) {
+  return rows * C < (1ll << 25) ? kBnMaxChunks / 2 : kBnMaxChunks;
+}
+
 void bn_shape(long long rows, int C, int &chunks, long long &rpc) {
   const int strips = C / 8 / bn_v(C);
-  long long want = (kBnMaxChunks + strips - 1) / strips;
+  const int maxc = bn_max_chunks(rows, C);
+  long long want = (maxc + strips - 1) / strips;
   if (want > (rows + 255) / 256) want = (rows + 255) / 256;  // >= 256 rows per chunk
   if (want < 1) want = 1;
   rpc = (rows + want - 1) / want;
@@ -211,13 +229,11 @@ __global__ __launch_bounds__(64 * kBnWaves) void bn_partial_kernel(const void *_
   for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
   const long long step = (long long)kBnWaves * rw;
   long long r = r0 + w * rw + rsub;
-  // four rows per iteration: their loads issue before any of them is consumed
-  for (; r + 3 * step < r1; r += 4 * step) {
+  // kBnUnroll rows per iteration: their loads issue before any of them is consumed
+  for (; r + (kBnUnroll - 1) * step < r1; r += kBnUnroll * step) {
     const long long e = r * C + col, es = step * C;
-    bn_accum<DT, MODE>(x, dy, y, e, k, slope, s0, s1);
-    bn_accum<DT, MODE>(x, dy, y, e + es, k, slope, s0, s1);
-    bn_accum<DT, MODE>(x, dy, y, e + 2 * es, k, slope, s0, s1);
-    bn_accum<DT, MODE>(x, dy, y, e + 3 * es, k, slope, s0, s1);
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) bn_accum<DT, MODE>(x, dy, y, e + u * es, k, slope, s0, s1);
   }
   for (; r < r1; r += step) bn_accum<DT, MODE>(x, dy, y, r * C + col, k, slope, s0, s1);
   for (int o = V; o < 64; o <<= 1)
@@ -413,10 +429,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const void *__restric
 }
 
 // the fused final (PCOPS_BN_FUSED_FINAL, default on; read per call so a test can compare both forms)
-// for strips of <= 128 channels: its [2][16][W8] double image fits the block's LDS
+// for strips of <= 64 channels: at 128 (C = 128) the last block's serial final cost more than
+// the launch it saves (profiles/r5_bn_variants.txt)
 bool bn_fuse(int C) {
   const char *e = getenv("PCOPS_BN_FUSED_FINAL");
-  return (!e || atoi(e) != 0) && bn_v(C) * 8 <= 128;
+  return (!e || atoi(e) != 0) && bn_v(C) * 8 <= 64;
 }
 
 unsigned bn_arrive_slots(int n) {   // host side: `n` consecutive counters no other launch in flight holds
