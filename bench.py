@@ -287,7 +287,7 @@ def kernel_work(name, a):
 # libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
             "attention bwd": "attn_(delta2|dkv3|dqs)_kernel",
-            "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream|wave)_kernel",
+            "attention bwd dkv": "attn_dkv[23]_kernel", "furthest_point_sampling": "fps_(reg|stream|wave|mw)_kernel",
             "furthest_point_sampling_counts": "fps_reg_kernel<[0-9]+, (true|false), true>",
             "chamfer_3D.forward": (r"chamfer_(nn|screen|mfma|cull|cull_prep)_kernel", r"chamfer_(nn|screen|mfma|cull)_kernel"), "knn": "knn", "layernorm_fwd": "ln_fwd_kernel",
             "layernorm_bwd": "ln_bwd_kernel", "attention bwd delta": "attn_delta_kernel",

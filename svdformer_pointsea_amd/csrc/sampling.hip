@@ -297,6 +297,101 @@ __global__ __launch_bounds__(64) void fps_wave_kernel(const float *__restrict__ 
   }
 }
 
+// NW waves per cloud, each lane holding R = T / (64 NW) reference threads (r = (w * 64 + lane) * R + j:
+// lane and wave order are r order) with PPL = R * PPT slots ordered by (j, i), as fps_wave_kernel: the
+// wave's winner is its lowest lane with the maximum, that lane's first slot; the waves' winners meet in
+// one LDS slot row (double buffered by round parity, ONE barrier), where the lowest wave with the
+// maximum wins -- the reference's order (distance, then smallest r, then smallest k).  Fewer waves than
+// fps_reg_kernel's one per 64 reference threads: a shorter cross-wave step for a longer sweep.  Used
+// for 512-thread clouds of 5-8 points per reference thread (2048 < N <= 4096): the model's 2304-point
+// merge 0.657 -> 0.585 us per round, 4096 equal; at 2048 points (4 per thread) the 8-wave kernel stays
+// ahead (0.576 vs 0.62), and 2-wave blocks lose everywhere (profiles/r5_fps_mw_ab.txt).
+template <int PPL, int NW>
+__global__ __launch_bounds__(64 * NW) void fps_mw_kernel(const float *__restrict__ xyz, int N, int M, int T, int L,
+                                                          int R, int PPT, int *__restrict__ idx,
+                                                          const int *__restrict__ counts) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float *p = xyz + (size_t)b * N * 3;
+  const int nb = counts ? min(max(counts[b], 0), N) : N;
+  int *out = idx + (size_t)b * M;
+  constexpr int kNeverBits = 0xBF800000;  // -1.0f
+  const int gl = w * 64 + lane;
+  typedef float fvec __attribute__((ext_vector_type(PPL)));
+  typedef int ivec __attribute__((ext_vector_type(PPL)));
+  fvec px, py, pz;   // register vectors: a uniform index extracts by movrel (fps_reg_kernel)
+  ivec tmp;
+#pragma unroll
+  for (int s = 0; s < PPL; ++s) {
+    const int j = s / PPT, i = s - j * PPT;
+    const int r = gl * R + j;
+    const int k = (int)bitrev_bits((unsigned)r, L) + T * i;
+    if (j < R && r < T && k < nb) {
+      px[s] = p[3 * k];
+      py[s] = p[3 * k + 1];
+      pz[s] = p[3 * k + 2];
+      const float mag = sqd3(px[s], py[s], pz[s]);
+      tmp[s] = ((double)mag <= 1e-3) ? kNeverBits : fbits(1e10f);  // sampling_gpu.cu:100-101
+    } else {
+      px[s] = py[s] = pz[s] = 0.f;
+      tmp[s] = kNeverBits;
+    }
+  }
+  __shared__ int sd[2][NW];       // per-wave maximum (float bits)
+  __shared__ float4 sc[2][NW];    // its point (x, y, z, k as int bits)
+  const float x0 = p[0], y0 = p[1], z0 = p[2];
+  float ox = x0, oy = y0, oz = z0;
+  if (threadIdx.x == 0 && M > 0) out[0] = 0;
+  for (int jr = 1; jr < M; ++jr) {
+    const int par = jr & 1;
+    int best = kNeverBits;
+#pragma unroll
+    for (int s = 0; s < PPL; ++s) {
+      int d = fbits(sqd3(px[s] - ox, py[s] - oy, pz[s] - oz));
+      if constexpr (PPL >= 16) asm volatile("" : "+v"(d));  // scalar chains (see fps_reg_kernel)
+      tmp[s] = min(d, tmp[s]);
+      best = max(best, tmp[s]);
+    }
+    const int wmax = wave_max_i32(best);
+    const uint64_t tied = __ballot(best == wmax);
+    const int wl = (int)__builtin_ctzll(tied);
+    int b0 = PPL - 1, b1 = PPL - 1;
+#pragma unroll
+    for (int s = PPL - 2; s >= 0; s -= 2) {
+      b0 = (tmp[s] == wmax) ? s : b0;
+      if (s >= 1) b1 = (tmp[s - 1] == wmax) ? s - 1 : b1;
+    }
+    const int wbi = __builtin_amdgcn_readlane(min(b0, b1), wl);
+    const float cx = px[wbi], cy = py[wbi], cz = pz[wbi];   // uniform index: outside the lane branch
+    if (lane == wl) {
+      const int j = wbi / PPT;
+      const int k = (int)bitrev_bits((unsigned)(gl * R + j), L) + T * (wbi - j * PPT);
+      sd[par][w] = wmax;
+      sc[par][w] = make_float4(cx, cy, cz, __int_as_float(k));
+    }
+    lds_barrier();
+    // every wave: the lowest wave holding the largest maximum (strict '>' in wave order)
+    int gd = sd[par][0], gw = 0;
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {
+      const int d = sd[par][q];
+      if (d > gd) {
+        gd = d;
+        gw = q;
+      }
+    }
+    int k;
+    if (gd != kNeverBits) {
+      const float4 c = sc[par][gw];
+      ox = c.x, oy = c.y, oz = c.z;
+      k = __float_as_int(c.w);
+    } else {  // no valid point at all: the reference's dists_i[0] == 0
+      ox = x0, oy = y0, oz = z0;
+      k = 0;
+    }
+    if (threadIdx.x == 0) out[jr] = k;
+  }
+}
+
 struct __align__(16) FpsSlot {
   float d, x, y, z;
   int k;
@@ -499,6 +594,30 @@ int fps_impl(const float *xyz, const int *counts, int B, int N, int M, int *idx,
       FPS_WAVE_CASE(32)   // larger register arrays spill (PPL 40: 496 B of scratch per lane)
     }
 #undef FPS_WAVE_CASE
+  }
+  {
+    // 4-wave blocks for 512-thread clouds of 5-8 points per reference thread (PCOPS_FPS_MW=0: off, A/B)
+    static const bool mw = [] {
+      const char *e = getenv("PCOPS_FPS_MW");
+      return !(e && e[0] == '0');
+    }();
+    if (mw && T == 512 && ppt >= 5 && ppt <= 8) {
+      constexpr int NW = 4;
+      const int R = T / (64 * NW);
+      const int ppl = R * ppt;
+#define FPS_MW_CASE(P)                                                                                        \
+  if (ppl <= P) {                                                                                             \
+    hipLaunchKernelGGL((fps_mw_kernel<P, NW>), dim3(B), dim3(64 * NW), 0, s, xyz, N, M, T, L, R, ppt, idx,   \
+                       counts);                                                                               \
+    PC_CHECK_LAUNCH();                                                                                        \
+    return PCOPS_OK;                                                                                          \
+  }
+      FPS_MW_CASE(10)
+      FPS_MW_CASE(12)
+      FPS_MW_CASE(14)
+      FPS_MW_CASE(16)
+#undef FPS_MW_CASE
+    }
   }
   if (ppt <= kFpsMaxPPT) {
     // clouds with > 16 points per reference thread use 2 hardware threads per

@@ -127,6 +127,33 @@ def test_fps_wave_kernel_edge_cases_bitexact(dev, kind):
     np.testing.assert_array_equal(got, O.furthest_point_sample(x, M))
 
 
+@pytest.mark.parametrize("kind", ["tiled2304", "zeros4000", "all_zero2500", "n2049", "tiled4096", "gauss3001"])
+def test_fps_mw_kernel_edge_cases_bitexact(dev, kind):
+    """The 4-wave kernel (512-thread clouds of 5-8 points per reference thread, fps_mw_kernel:
+    2048 < N <= 4096) on the inputs that stress its tie order across lanes, slots and waves:
+    duplicated points with more samples than distinct points (the tie order alone decides),
+    skipped near-origin points, an all-zero cloud, N = 2049 (the first size it takes) and 4096."""
+    from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample
+
+    rng = np.random.default_rng(200 + len(kind))
+    if kind == "tiled2304":
+        x, M = _tiled(rng, 3, 300, 2304), 1024
+    elif kind == "tiled4096":
+        x, M = _tiled(rng, 2, 500, 4096), 1024
+    elif kind == "zeros4000":
+        x, M = (rng.random((2, 4000, 3)) - 0.5).astype(np.float32), 3000
+        x[:, -700:] = 0.0
+        x[:, 50:90] = 1e-2   # |p|^2 = 3e-4 <= 1e-3: skipped
+    elif kind == "all_zero2500":
+        x, M = np.zeros((2, 2500, 3), np.float32), 40
+    elif kind == "n2049":
+        x, M = (rng.random((2, 2049, 3)) - 0.5).astype(np.float32), 700
+    else:
+        x, M = (rng.standard_normal((3, 3001, 3)) * 0.45).astype(np.float32), 777
+    got = furthest_point_sample(T(x, dev), M).cpu().numpy()
+    np.testing.assert_array_equal(got, O.furthest_point_sample(x, M))
+
+
 def test_fps_full_size_properties(dev):
     """B=32, 16384 -> 2048 (the loss FPS): size-independent properties."""
     from svdformer_pointsea_amd.pointnet2_utils import furthest_point_sample

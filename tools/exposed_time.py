@@ -2,14 +2,14 @@
 part of the group's busy time during which NO other kernel runs anywhere on the GPU (what the step
 would lose if the group took zero time and everything else stayed put), next to its total kernel
 time and the part that runs with the main stream idle.
-    python tools/exposed_time.py <kernel_trace.csv[.gz]> <steps> [regex=fps_(reg|wave|stream)_kernel]"""
+    python tools/exposed_time.py <kernel_trace.csv[.gz]> <steps> [regex=fps_(reg|wave|stream|mw)_kernel]"""
 import csv
 import gzip
 import re
 import sys
 
 path, steps = sys.argv[1], int(sys.argv[2])
-pat = re.compile(sys.argv[3] if len(sys.argv) > 3 else r"fps_(reg|wave|stream)_kernel")
+pat = re.compile(sys.argv[3] if len(sys.argv) > 3 else r"fps_(reg|wave|stream|mw)_kernel")
 rows = list(csv.DictReader((gzip.open if path.endswith(".gz") else open)(path, "rt")))
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
 marks = [i for i, e in enumerate(ev) if "spin_kernel" in e[2]]
