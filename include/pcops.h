@@ -169,6 +169,14 @@ int pcops_chamfer_forward_ws(const float *xyz1, const float *xyz2, int B, int N,
 int pcops_chamfer_backward(const float *xyz1, const float *xyz2, int B, int N, int M, const float *graddist1,
                            const float *graddist2, const int *idx1, const int *idx2, float *gradxyz1, float *gradxyz2,
                            pcops_stream_t stream);
+/* pcops_chamfer_sqrt_mean_grad: the distance gradients of the sqrt-mean Chamfer losses
+ * (utils/loss_utils.py:10-31 chamfer_sqrt / chamfer_single_side_sqrt: torch.sqrt, torch.mean and
+ * "/ 2" on dist1 / dist2) in autograd's order, from the loss gradient grad_out (one float on the
+ * device), scale (0.5 for chamfer_sqrt, 1 single-sided) and the forward's s = sqrt(dist) (n1 / n2
+ * elements; s2 NULL: gd2 = 0):  gd = ((g * scale) * (1 / n)) / (2 s).  Feeds pcops_chamfer_backward;
+ * replaces the autograd chain between the loss and chamfer_3D.backward (dist_chamfer_3D.py:56-60). */
+int pcops_chamfer_sqrt_mean_grad(const float *grad_out, float scale, const float *s1, long long n1, const float *s2,
+                                 long long n2, float *gd1, float *gd2, pcops_stream_t stream);
 
 /* ---------------- EMD (metrics/EMD) ----------------
  * emd.forward(xyz1, xyz2, dist, assignment, price, assignment_inv, bid, bid_increments,

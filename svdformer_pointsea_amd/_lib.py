@@ -47,6 +47,7 @@ _SIGS = {
     "pcops_chamfer_workspace_bytes": (ULL, [I, I, I]),
     "pcops_chamfer_forward_ws": (I, [P, P, I, I, I, P, P, P, P, P, ULL, P]),
     "pcops_chamfer_backward": (I, [P, P, I, I, I, P, P, P, P, P, P, P]),
+    "pcops_chamfer_sqrt_mean_grad": (I, [P, F, P, LL, P, LL, P, P, P]),
     "pcops_emd_workspace_bytes": (ULL, [I, I]),
     "pcops_emd_forward": (I, [P, P, I, I, F, I, P, P, P, ULL, P]),
     "pcops_emd_backward": (I, [P, P, P, P, I, I, P, P]),

@@ -14,29 +14,35 @@ from torch.amp import custom_bwd, custom_fwd
 from ._lib import Workspace, call, lib, ptr, require_float, stream_of
 
 
+def chamfer_forward_raw(xyz1, xyz2):
+    """(dist1, dist2, idx1, idx2) of two fp32 clouds on libpcops, outside autograd."""
+    require_float(xyz1, "xyz1")
+    require_float(xyz2, "xyz2")
+    B, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    dev = xyz1.device
+    dist1 = torch.empty(B, n, device=dev)
+    dist2 = torch.empty(B, m, device=dev)
+    idx1 = torch.empty(B, n, dtype=torch.int32, device=dev)
+    idx2 = torch.empty(B, m, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        # large clouds: the spatially culled search (scratch for the sorted clouds and tile boxes)
+        wsb = lib().pcops_chamfer_workspace_bytes(B, n, m)
+        if wsb:
+            ws = Workspace.get(dev, wsb)
+            call("chamfer_3D.forward", lib().pcops_chamfer_forward_ws, ptr(xyz1), ptr(xyz2), B, n, m,
+                 ptr(dist1), ptr(dist2), ptr(idx1), ptr(idx2), ptr(ws), wsb, stream_of(xyz1))
+        else:
+            call("chamfer_3D.forward", lib().pcops_chamfer_forward, ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist1),
+                 ptr(dist2), ptr(idx1), ptr(idx2), stream_of(xyz1))
+    return dist1, dist2, idx1, idx2
+
+
 class chamfer_3DFunction(Function):
     @staticmethod
     @custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, xyz1, xyz2):
-        require_float(xyz1, "xyz1")
-        require_float(xyz2, "xyz2")
-        B, n, _ = xyz1.shape
-        m = xyz2.shape[1]
-        dev = xyz1.device
-        dist1 = torch.empty(B, n, device=dev)
-        dist2 = torch.empty(B, m, device=dev)
-        idx1 = torch.empty(B, n, dtype=torch.int32, device=dev)
-        idx2 = torch.empty(B, m, dtype=torch.int32, device=dev)
-        with torch.cuda.device(dev):
-            # large clouds: the spatially culled search (scratch for the sorted clouds and tile boxes)
-            wsb = lib().pcops_chamfer_workspace_bytes(B, n, m)
-            if wsb:
-                ws = Workspace.get(dev, wsb)
-                call("chamfer_3D.forward", lib().pcops_chamfer_forward_ws, ptr(xyz1), ptr(xyz2), B, n, m,
-                     ptr(dist1), ptr(dist2), ptr(idx1), ptr(idx2), ptr(ws), wsb, stream_of(xyz1))
-            else:
-                call("chamfer_3D.forward", lib().pcops_chamfer_forward, ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist1),
-                     ptr(dist2), ptr(idx1), ptr(idx2), stream_of(xyz1))
+        dist1, dist2, idx1, idx2 = chamfer_forward_raw(xyz1, xyz2)
         ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
         ctx.mark_non_differentiable(idx1, idx2)
         return dist1, dist2, idx1, idx2

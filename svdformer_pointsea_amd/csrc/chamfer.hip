@@ -1285,6 +1285,41 @@ extern "C" int pcops_chamfer_forward_ws(const float *xyz1, const float *xyz2, in
   return PCOPS_OK;
 }
 
+// d(loss)/d(dist) of the reference's sqrt-mean Chamfer losses (loss_utils.py: chamfer_sqrt =
+// (mean(sqrt(d1)) + mean(sqrt(d2))) / 2, chamfer_single_side_sqrt = mean(sqrt(d1))) in one launch,
+// in autograd's own order: t = g * scale (DivBackward of "/ 2", a multiply by 0.5; 1 single-sided),
+// t * (1 / n) (MeanBackward: torch divides by a CPU scalar as a multiply by its fp32 reciprocal),
+// then / (2 * sqrt(d)) (SqrtBackward) -- bitwise the gradient autograd hands chamfer_3D.backward.
+// s2 == nullptr: the second direction takes no gradient (zeros, as for an unused output).
+__global__ void chamfer_sqm_grad_kernel(const float *__restrict__ go, float scale, const float *__restrict__ s1,
+                                        long long n1, float inv1, const float *__restrict__ s2, long long n2,
+                                        float inv2, float *__restrict__ gd1, float *__restrict__ gd2) {
+  const float t = go[0] * scale;
+  const float t1 = t * inv1, t2 = t * inv2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n1 + n2; i += stride) {
+    if (i < n1)
+      gd1[i] = t1 / (2.f * s1[i]);
+    else
+      gd2[i - n1] = s2 ? t2 / (2.f * s2[i - n1]) : 0.f;
+  }
+}
+
+extern "C" int pcops_chamfer_sqrt_mean_grad(const float *grad_out, float scale, const float *s1, long long n1,
+                                            const float *s2, long long n2, float *gd1, float *gd2,
+                                            pcops_stream_t stream) {
+  if (n1 < 0 || n2 < 0) return PCOPS_ERR_INVALID;
+  if (n1 + n2 == 0) return PCOPS_OK;
+  if (!grad_out || (n1 && (!s1 || !gd1)) || (n2 && !gd2)) return PCOPS_ERR_INVALID;
+  const float inv1 = n1 ? 1.0f / (float)n1 : 0.f, inv2 = n2 ? 1.0f / (float)n2 : 0.f;
+  long long blocks = (n1 + n2 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(chamfer_sqm_grad_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, grad_out,
+                     scale, s1, n1, inv1, s2, n2, inv2, gd1, gd2);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
 extern "C" int pcops_chamfer_backward(const float *xyz1, const float *xyz2, int B, int N, int M,
                                       const float *graddist1, const float *graddist2, const int *idx1,
                                       const int *idx2, float *gradxyz1, float *gradxyz2, pcops_stream_t stream) {

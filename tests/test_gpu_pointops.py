@@ -371,6 +371,40 @@ def test_chamfer_backward_deterministic(dev, case):
             np.testing.assert_allclose(got[fin], ora[fin], rtol=1e-5, atol=1e-6 * scale)
 
 
+@pytest.mark.parametrize("B,N,M,kind", [(2, 512, 600, "gauss"), (3, 2048, 2048, "gauss"), (2, 700, 900, "dup"),
+                                        (2, 16384, 16384, "gauss"), (4, 2048, 16384, "gauss")])
+def test_sqrt_mean_loss_fused_bitwise(dev, monkeypatch, B, N, M, kind):
+    """chamfer_sqrt / chamfer_single_side_sqrt / get_loss as one autograd node (the distance
+    gradient formed in one launch, pcops_chamfer_sqrt_mean_grad) against the autograd chain
+    (PCOPS_LOSS_FUSED=0): loss values and both clouds' gradients bitwise equal, including
+    coincident points (sqrt(d) = 0: an infinite distance gradient either way) and the culled
+    search's sizes."""
+    from svdformer_pointsea_amd import metrics
+
+    g = torch.Generator().manual_seed(B * N + M)
+    a = torch.randn(B, N, 3, generator=g) * 0.45
+    b = torch.randn(B, M, 3, generator=g) * 0.45
+    if kind == "dup":
+        b[:, :N // 2] = a[:, :N // 2]    # half of a's points have an exact partner
+    res = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("PCOPS_LOSS_FUSED", fused)
+        out = []
+        for fn in (metrics.chamfer_sqrt, metrics.chamfer_single_side_sqrt):
+            x, y = a.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+            loss = fn(x, y)
+            gx, gy = torch.autograd.grad(loss * 3.0, (x, y))
+            out += [loss.detach(), gx, gy]
+        x, y, z = (b[:, :N // 4].to(dev).contiguous().requires_grad_(True),
+                   b[:, :N // 2].to(dev).contiguous().requires_grad_(True), b.to(dev).requires_grad_(True))
+        gt = a.to(dev)
+        loss, parts = metrics.get_loss([x, y, z], gt, sqrt=True, alpha1=1, alpha2=0.5)
+        out += [loss.detach(), *[p.detach() for p in parts], *torch.autograd.grad(loss, (x, y, z))]
+        res[fused] = out
+    for u, v in zip(res["0"], res["1"]):
+        torch.testing.assert_close(u, v, rtol=0, atol=0, equal_nan=True)
+
+
 def test_chamfer_backward_outlier_block_bound(dev):
     """one large partner term sets the fixed-point scale of every target in
     its block, so a target with small terms gets absolute, not relative, resolution.

@@ -1,8 +1,9 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
-# stages are tools/gpu_run.sh's).  This is the last one run: the late-round-5 full pass.
+# stages are tools/gpu_run.sh's).  This is the last one run.
 set -o pipefail
-O=gpurun_out/r5fin; mkdir -p $O; export TMPDIR=/tmp
-bash tools/gpu_run.sh $O tests smoke bench trace || exit 1
-tail -3 $O/pytest_gpu.log; cat $O/smoke.log | tail -2
-python -c "import json;d=json.load(open('$O/bench.json'));print(d['ms_per_step'],d['value'],d['pointsea_train_step'].get('ms_per_step') if isinstance(d.get('pointsea_train_step'),dict) else None)"
-cat $O/trace_window.txt | head -3
+O=gpurun_out/r5lf; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_pointops.py tests/test_gpu_model.py tests/test_gpu_train_step.py tests/test_gpu_pointsea.py > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+export BENCH_AB="X=1;PCOPS_LOSS_FUSED=0;X=1;PCOPS_LOSS_FUSED=0"
+bash tools/gpu_run.sh $O bench_ab || exit 1
+grep -E '^==|ms_per_step' $O/bench_ab.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
