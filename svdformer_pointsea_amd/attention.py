@@ -385,6 +385,28 @@ def attention_core(q, k, v, heads, scale=None, batch_first=False):
     return AttentionCore.apply((heads, scale, E, batch_first, *wins), *srcs)
 
 
+class _RowSplit(Function):
+    """(t[c0:c1], t[c1:c2], ...) of a parameter along dim 0, as separate outputs; the backward
+    concatenates the blocks' gradients (zeros for a block that received none) into the parameter's
+    gradient in one launch.  The values are exactly those of per-slice SliceBackward + accumulation
+    (disjoint blocks: every element is one block's gradient)."""
+
+    @staticmethod
+    def forward(ctx, t, cuts):
+        ctx.cuts = cuts
+        return tuple(t[a:b] for a, b in zip(cuts[:-1], cuts[1:]))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ref = next(g for g in gs if g is not None)
+        parts = [torch.zeros((b - a,) + tuple(ref.shape[1:]), dtype=ref.dtype, device=ref.device) if g is None else g
+                 for g, a, b in zip(gs, ctx.cuts[:-1], ctx.cuts[1:])]
+        return torch.cat(parts, 0), None
+
+
+_ROW_SPLIT = os.environ.get("PCOPS_ROW_SPLIT", "1") != "0"   # A/B switch: packed in_proj row blocks by _RowSplit
+
+
 class MultiheadAttention(nn.Module):
     """nn.MultiheadAttention(embed_dim, num_heads) subset used by the reference:
     no masks, dropout 0, returns (output, None); seq-first by default like
@@ -411,28 +433,37 @@ class MultiheadAttention(nn.Module):
             nn.init.constant_(self.in_proj_bias, 0.0)
             nn.init.constant_(self.out_proj.bias, 0.0)
 
-    def _proj(self, x, r0, r1):
-        # the whole packed weight unsliced: a [0:3E] slice cost a SliceBackward (a
-        # full-size zero fill + copy) per weight and bias every step
-        full = (r0, r1) == (0, self.in_proj_weight.shape[0])
-        w = self.in_proj_weight if full else self.in_proj_weight[r0:r1]
-        b = None if self.in_proj_bias is None else (self.in_proj_bias if full else self.in_proj_bias[r0:r1])
-        return linear(x, w, b)
+    def _projs(self, xs, cuts):
+        """The in-projections of the inputs xs by the packed weight's row blocks [cuts[i], cuts[i+1]).
+        One input: the whole packed weight unsliced.  Several: the row blocks come from _RowSplit,
+        whose backward assembles the weight's (and bias's) gradient in one concatenation -- a
+        plain slice per block cost a SliceBackward (full-size zero fill + copy) per block and an
+        accumulating add, for the weight and for the bias, every step."""
+        if len(xs) == 1:
+            return (linear(xs[0], self.in_proj_weight, self.in_proj_bias),)
+        ws = _RowSplit.apply(self.in_proj_weight, cuts) if _ROW_SPLIT else tuple(
+            self.in_proj_weight[a:b] for a, b in zip(cuts[:-1], cuts[1:]))
+        if self.in_proj_bias is None:
+            bs = (None,) * len(xs)
+        else:
+            bs = _RowSplit.apply(self.in_proj_bias, cuts) if _ROW_SPLIT else tuple(
+                self.in_proj_bias[a:b] for a, b in zip(cuts[:-1], cuts[1:]))
+        return tuple(linear(x, w, b) for x, w, b in zip(xs, ws, bs))
 
     def forward(self, query, key, value, need_weights=True):
         E, H = self.embed_dim, self.num_heads
         scale = 1.0 / math.sqrt(self.head_dim)
         if query is key and key is value:
-            srcs = (self._proj(query, 0, 3 * E),)
+            srcs = self._projs((query,), (0, 3 * E))
             wins = ((0, 0), (0, E), (0, 2 * E))
         elif query is key:
-            srcs = (self._proj(query, 0, 2 * E), self._proj(value, 2 * E, 3 * E))
+            srcs = self._projs((query, value), (0, 2 * E, 3 * E))
             wins = ((0, 0), (0, E), (1, 0))
         elif key is value:
-            srcs = (self._proj(query, 0, E), self._proj(key, E, 3 * E))
+            srcs = self._projs((query, key), (0, E, 3 * E))
             wins = ((0, 0), (1, 0), (1, E))
         else:
-            srcs = (self._proj(query, 0, E), self._proj(key, E, 2 * E), self._proj(value, 2 * E, 3 * E))
+            srcs = self._projs((query, key, value), (0, E, 2 * E, 3 * E))
             wins = ((0, 0), (1, 0), (2, 0))
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
         if dt is not None and any(s.dtype != dt for s in srcs):

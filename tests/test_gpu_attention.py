@@ -681,6 +681,37 @@ def test_layernorm_fused_bias_colsum(dev, monkeypatch, amp):
         torch.testing.assert_close(g_fus[n], g_ref[n], **tol, msg=n)
 
 
+@pytest.mark.parametrize("mode", ["kv", "qk", "all"])
+def test_in_proj_row_split_bitwise(dev, monkeypatch, mode):
+    """The packed in_proj weight / bias taken in row blocks through _RowSplit (one concatenation
+    assembles their gradients) against plain slices (SliceBackward + accumulation), bf16 autocast as
+    in the step: output and every gradient bitwise equal."""
+    from svdformer_pointsea_amd import attention as A
+
+    torch.manual_seed(7)
+    E, H, L, S, B = 256, 4, 96, 130, 3
+    mha = A.MultiheadAttention(E, H, batch_first=True).to(dev)
+    with torch.no_grad():
+        mha.in_proj_bias.normal_()
+    q = torch.randn(B, L, E, device=dev)
+    k = torch.randn(B, S, E, device=dev)
+    v = torch.randn(B, S if mode != "qk" else L, E, device=dev)
+    g = torch.randn(B, L, E, device=dev)
+    res = {}
+    for split in (False, True):
+        monkeypatch.setattr(A, "_ROW_SPLIT", split)
+        mha.zero_grad(set_to_none=True)
+        xs = [t.clone().requires_grad_(True) for t in (q, k, v)]
+        qq, kk, vv = xs
+        args = {"kv": (qq, kk, kk), "qk": (qq, qq, vv), "all": (qq, kk, vv)}[mode]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            o, _ = mha(*args)
+        o.float().backward(g)
+        res[split] = [o.detach(), mha.in_proj_weight.grad, mha.in_proj_bias.grad] + [x.grad for x in xs if x.grad is not None]
+    for u, w in zip(res[False], res[True]):
+        assert torch.equal(u, w), (u.float() - w.float()).abs().max().item()
+
+
 def test_fused_bias_sum_in_bias_dtype_bitwise(dev, monkeypatch):
     """With bf16 biases (bench.py's FlatParams shadows) the fused bias sums of the LayerNorm and GELU
     backwards are stored in bf16 by the summing launch itself (round 5), so the Linear backward takes
