@@ -167,6 +167,27 @@ class MLP_CONV(nn.Module):
         return self.mlp(x)
 
 
+class _ChannelMean(torch.autograd.Function):
+    """x.mean(dim=1) whose backward hands autograd the broadcast gradient as an expanded view of the
+    small (B, 1, S, K) grad / C instead of materialising the full-size (B, C, S, K) quotient: the
+    same values element for element (torch divides by the count as a multiply by its reciprocal,
+    either side of the broadcast), and the add that sums it with the PCSA input gradient reads the
+    broadcast directly.  The materialised form cost two strided copies over the channels_last
+    activation per module (~0.28 ms per PCN step in the replay trace)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x.mean(dim=1)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g / ctx.shape[1]).unsqueeze(1).expand(ctx.shape)
+
+
+_CHANNEL_MEAN = _os.environ.get("PCOPS_CHANNEL_MEAN", "1") != "0"   # A/B switch
+
+
 class _PCSAApply(torch.autograd.Function):
     """PCSA's DCT -> gate -> inverse-DCT chain (model_utils.py:413-430) as one
     libpcops pass per patch on the channels_last (B, C, S, K) features."""
@@ -237,7 +258,7 @@ class PCSA(nn.Module):
         if (x.is_cuda and K in (4, 8, 16, 32) and x.dtype in (torch.float32, torch.bfloat16)
                 and x.is_contiguous(memory_format=torch.channels_last)):
             # one pass per (b, s) patch on libpcops (csrc/pcsa.hip): out = D^T diag(g) D x
-            gates = self.freq_mlp(x.mean(dim=1))
+            gates = self.freq_mlp(_ChannelMean.apply(x) if _CHANNEL_MEAN else x.mean(dim=1))
             return _PCSAApply.apply(x, gates, dct)
         x_flat = x.permute(0, 2, 1, 3).contiguous().view(B * S * C, K)
         spec = torch.matmul(x_flat, dct.t())

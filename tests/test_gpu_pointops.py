@@ -714,6 +714,32 @@ def test_pcsa_kernel_matches_torch_chain(dev, dtype, K, C):
         torch.testing.assert_close(a.float(), b.float(), rtol=tol * 5, atol=tol * 5)
 
 
+@pytest.mark.parametrize("dtype,K,C", [(torch.bfloat16, 16, 128), (torch.float32, 8, 64)])
+def test_pcsa_channel_mean_broadcast_grad_bitwise(dev, monkeypatch, dtype, K, C):
+    """PCSA's gate input x.mean(dim=1) through _ChannelMean (the backward hands autograd the
+    broadcast gradient as an expanded view of grad / C) against torch's MeanBackward, which
+    materialises it: output, input gradient and parameter gradients bitwise equal."""
+    import svdformer_pointsea_amd.svdformer as SV
+
+    torch.manual_seed(K * C)
+    m = SV.PCSA(C, K).to(dev)
+    B, S = 3, 41
+    x0 = torch.randn(B, C, S, K, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+    go = torch.randn(B, C, S, K, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+    amp = dtype == torch.bfloat16
+    res = {}
+    for on in (False, True):
+        monkeypatch.setattr(SV, "_CHANNEL_MEAN", on)
+        m.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            y = m(x)
+        y.backward(go.to(y.dtype))
+        res[on] = [y.detach(), x.grad] + [p.grad for p in m.parameters()]
+    for u, v in zip(res[False], res[True]):
+        assert torch.equal(u, v), (u.float() - v.float()).abs().max().item()
+
+
 @pytest.mark.parametrize("B,S,N,C,K,pad,kind", [(32, 512, 512, 64, 8, 0, "rand"), (16, 1024, 1024, 256, 4, 0, "rand"),
                                                  (16, 1024, 1024, 64, 8, 0, "tiled"), (2, 300, 300, 40, 5, 2, "rand"),
                                                  (3, 200, 777, 128, 20, 1, "tiled"), (2, 1000, 100, 32, 16, 0, "rand"),
