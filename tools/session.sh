@@ -1,9 +1,9 @@
 # Scratch GPU session for `gpurun -- bash tools/session.sh` (overwritten for each session; the
-# stages are tools/gpu_run.sh's).  This is the last one run.
+# stages are tools/gpu_run.sh's).  This is the last one run: the round-5 closing full pass.
 set -o pipefail
-O=gpurun_out/r5cm; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_pointops.py tests/test_gpu_model.py tests/test_gpu_train_step.py tests/test_gpu_pointsea.py tests/test_gpu_sa_fused.py > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
-tail -1 $O/pytest.log
-export BENCH_AB="X=1;PCOPS_CHANNEL_MEAN=0;X=1;PCOPS_CHANNEL_MEAN=0"
-bash tools/gpu_run.sh $O bench_ab || exit 1
-grep -E '^==|ms_per_step' $O/bench_ab.txt | sed 's/.*"ms_per_step": \([0-9.]*\).*/\1/' | paste - -
+O=gpurun_out/r5fin2; mkdir -p $O; export TMPDIR=/tmp
+bash tools/gpu_run.sh $O tests smoke bench trace || exit 1
+tail -2 $O/pytest_gpu.log; tail -1 $O/smoke.log
+python -c "import json;d=json.load(open('$O/bench.json'));print(d['ms_per_step'],d['value'],d['pointsea_train_step'].get('ms_per_step'))"
+head -2 $O/trace_window.txt
+timeout -k 10 400 python tools/glue_sites.py --nodes > $O/glue_nodes.txt 2> $O/glue_nodes.err || true
