@@ -178,6 +178,18 @@ int pcops_chamfer_backward(const float *xyz1, const float *xyz2, int B, int N, i
 int pcops_chamfer_sqrt_mean_grad(const float *grad_out, float scale, const float *s1, long long n1, const float *s2,
                                  long long n2, float *gd1, float *gd2, pcops_stream_t stream);
 
+/* ---------------- 3x3 / stride 2 / pad 1 max pool (torchvision resnet stem, PointSea ResEncoder)
+ * pcops_maxpool3s2_fwd: nn.MaxPool2d(3, 2, 1) on a channels_last (N, H, W, C) activation (dtype 0
+ * fp32, 1 bf16) -> y (N, ceil(H/2), ceil(W/2), C) and each output's winning window offset (uint8,
+ * 3 i + j), torch's NHWC rule (first maximum, a NaN takes the slot).  pcops_maxpool3s2_bwd: the
+ * input gradient, per element the gradients of the windows it won summed in fp32 in (ph, pw) order
+ * (max_pool_backward_nhwc).  Replaces torch's max_pool2d_with_indices(_backward) for that pool
+ * (models_PointSea/PointSea.py:37-61, torchvision resnet18 maxpool). */
+int pcops_maxpool3s2_fwd(const void *x, int dtype, int N, int H, int W, int C, void *y, unsigned char *argmax,
+                         pcops_stream_t stream);
+int pcops_maxpool3s2_bwd(const void *gy, const unsigned char *argmax, int dtype, int N, int H, int W, int C, void *gx,
+                         pcops_stream_t stream);
+
 /* ---------------- EMD (metrics/EMD) ----------------
  * emd.forward(xyz1, xyz2, dist, assignment, price, assignment_inv, bid, bid_increments,
  *             max_increments, unass_idx, unass_cnt, unass_cnt_sum, cnt_tmp, max_idx, eps, iters):

@@ -48,6 +48,8 @@ _SIGS = {
     "pcops_chamfer_forward_ws": (I, [P, P, I, I, I, P, P, P, P, P, ULL, P]),
     "pcops_chamfer_backward": (I, [P, P, I, I, I, P, P, P, P, P, P, P]),
     "pcops_chamfer_sqrt_mean_grad": (I, [P, F, P, LL, P, LL, P, P, P]),
+    "pcops_maxpool3s2_fwd": (I, [P, I, I, I, I, I, P, P, P]),
+    "pcops_maxpool3s2_bwd": (I, [P, P, I, I, I, I, I, P, P]),
     "pcops_emd_workspace_bytes": (ULL, [I, I]),
     "pcops_emd_forward": (I, [P, P, I, I, F, I, P, P, P, ULL, P]),
     "pcops_emd_backward": (I, [P, P, P, P, I, I, P, P]),

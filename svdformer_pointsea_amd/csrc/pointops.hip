@@ -600,3 +600,227 @@ extern "C" int pcops_edge_group_grad(const void *grad_out, int grad_dtype, const
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
+
+// ---- 3x3 / stride 2 / pad 1 max pool on channels_last (N, H, W, C) bf16 / fp32 activations
+// (torchvision's resnet stem pool, models_PointSea/PointSea.py:37-61 ResEncoder).  Forward: torch's
+// NHWC kernel's rule -- the window scanned row by row, strict '>' keeps the first maximum, a NaN
+// always takes the slot (so the last NaN wins) -- and the winner's window offset (0..8) as uint8.
+// Backward: per input element the gradients of the windows whose winner it is, summed in fp32 over
+// (ph, pw) ascending as torch's max_pool_backward_nhwc does, stored once (no atomics, no zero fill).
+namespace {
+template <typename T>
+__global__ void maxpool3s2_fwd_kernel(const T *__restrict__ x, int N, int H, int W, int C, int OH, int OW,
+                                      T *__restrict__ y, unsigned char *__restrict__ arg) {
+  const long long total = (long long)N * OH * OW * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    long long r = e / C;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    float best = -INFINITY;
+    int bi = -1, first = -1;
+    for (int i = 0; i < 3; ++i) {
+      const int ih = 2 * oh - 1 + i;
+      if (ih < 0 || ih >= H) continue;
+      for (int j = 0; j < 3; ++j) {
+        const int iw = 2 * ow - 1 + j;
+        if (iw < 0 || iw >= W) continue;
+        if (first < 0) first = 3 * i + j;
+        const float v = (float)x[(((long long)n * H + ih) * W + iw) * C + c];
+        if (v > best || v != v) {
+          best = v;
+          bi = 3 * i + j;
+        }
+      }
+    }
+    // a window of -inf only: torch keeps its initial index 0 (image element (0, 0)); here the
+    // window's first element (unreachable after the ReLU this pool follows)
+    if (bi < 0) bi = first;
+    y[e] = (T)best;
+    arg[e] = (unsigned char)bi;
+  }
+}
+
+template <typename T>
+__global__ void maxpool3s2_bwd_kernel(const T *__restrict__ gy, const unsigned char *__restrict__ arg, int N, int H,
+                                      int W, int C, int OH, int OW, T *__restrict__ gx) {
+  const long long total = (long long)N * H * W * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    long long r = e / C;
+    const int iw = (int)(r % W);
+    r /= W;
+    const int ih = (int)(r % H);
+    const int n = (int)(r / H);
+    // windows (ph, pw) with 2 ph - 1 <= ih <= 2 ph + 1 (torch's p_start / p_end for k 3, s 2, p 1)
+    const int ph0 = ih + 1 < 3 ? 0 : (ih + 1 - 3) / 2 + 1, ph1 = min((ih + 1) / 2 + 1, OH);
+    const int pw0 = iw + 1 < 3 ? 0 : (iw + 1 - 3) / 2 + 1, pw1 = min((iw + 1) / 2 + 1, OW);
+    float acc = 0.f;
+    for (int ph = ph0; ph < ph1; ++ph)
+      for (int pw = pw0; pw < pw1; ++pw) {
+        const long long o = (((long long)n * OH + ph) * OW + pw) * C + c;
+        const int a = arg[o];
+        if (2 * ph - 1 + a / 3 == ih && 2 * pw - 1 + a % 3 == iw) acc += (float)gy[o];
+      }
+    gx[e] = (T)acc;
+  }
+}
+
+// 8 channels per thread (C % 8 == 0): 16-byte (bf16) / 32-byte (fp32) window loads and stores, the
+// same per-channel rule as the scalar kernels above
+template <typename T>
+struct PoolVec8 {
+  T v[8];
+};
+
+template <typename T>
+__global__ void maxpool3s2_fwd8_kernel(const T *__restrict__ x, int N, int H, int W, int C, int OH, int OW,
+                                       T *__restrict__ y, unsigned char *__restrict__ arg) {
+  const int C8 = C / 8;
+  const long long total = (long long)N * OH * OW * C8;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C8) * 8;
+    long long r = e / C8;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) best[k] = -INFINITY, bi[k] = -1;
+    int first = -1;
+    for (int i = 0; i < 3; ++i) {
+      const int ih = 2 * oh - 1 + i;
+      if (ih < 0 || ih >= H) continue;
+      for (int j = 0; j < 3; ++j) {
+        const int iw = 2 * ow - 1 + j;
+        if (iw < 0 || iw >= W) continue;
+        if (first < 0) first = 3 * i + j;
+        const PoolVec8<T> t = *reinterpret_cast<const PoolVec8<T> *>(x + (((long long)n * H + ih) * W + iw) * C + c);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float v = (float)t.v[k];
+          if (v > best[k] || v != v) {
+            best[k] = v;
+            bi[k] = 3 * i + j;
+          }
+        }
+      }
+    }
+    PoolVec8<T> o;
+    unsigned long long a = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o.v[k] = (T)best[k];
+      a |= (unsigned long long)(unsigned char)(bi[k] < 0 ? first : bi[k]) << (8 * k);
+    }
+    const long long oe = (((long long)n * OH + oh) * OW + ow) * C + c;
+    *reinterpret_cast<PoolVec8<T> *>(y + oe) = o;
+    *reinterpret_cast<unsigned long long *>(arg + oe) = a;
+  }
+}
+
+template <typename T>
+__global__ void maxpool3s2_bwd8_kernel(const T *__restrict__ gy, const unsigned char *__restrict__ arg, int N, int H,
+                                       int W, int C, int OH, int OW, T *__restrict__ gx) {
+  const int C8 = C / 8;
+  const long long total = (long long)N * H * W * C8;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C8) * 8;
+    long long r = e / C8;
+    const int iw = (int)(r % W);
+    r /= W;
+    const int ih = (int)(r % H);
+    const int n = (int)(r / H);
+    const int ph0 = ih + 1 < 3 ? 0 : (ih + 1 - 3) / 2 + 1, ph1 = min((ih + 1) / 2 + 1, OH);
+    const int pw0 = iw + 1 < 3 ? 0 : (iw + 1 - 3) / 2 + 1, pw1 = min((iw + 1) / 2 + 1, OW);
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int ph = ph0; ph < ph1; ++ph)
+      for (int pw = pw0; pw < pw1; ++pw) {
+        const long long o = (((long long)n * OH + ph) * OW + pw) * C + c;
+        const int want = 3 * (ih - 2 * ph + 1) + (iw - 2 * pw + 1);   // this element's offset in window (ph, pw)
+        const unsigned long long a = *reinterpret_cast<const unsigned long long *>(arg + o);
+        const PoolVec8<T> g = *reinterpret_cast<const PoolVec8<T> *>(gy + o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if ((int)((a >> (8 * k)) & 0xFF) == want) acc[k] += (float)g.v[k];
+      }
+    PoolVec8<T> out;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out.v[k] = (T)acc[k];
+    *reinterpret_cast<PoolVec8<T> *>(gx + (((long long)n * H + ih) * W + iw) * C + c) = out;
+  }
+}
+
+unsigned pool_grid(long long total) {
+  long long g = (total + 255) / 256;
+  return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+}  // namespace
+
+extern "C" int pcops_maxpool3s2_fwd(const void *x, int dtype, int N, int H, int W, int C, void *y,
+                                    unsigned char *argmax, pcops_stream_t stream) {
+  if (N < 0 || H < 0 || W < 0 || C < 0 || (dtype != 0 && dtype != 1)) return PCOPS_ERR_INVALID;
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;   // floor((H + 2 - 3) / 2) + 1
+  const long long total = (long long)N * OH * OW * C;
+  if (total == 0) return PCOPS_OK;
+  if (!x || !y || !argmax) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (C % 8 == 0 && ((uintptr_t)x | (uintptr_t)y) % 16 == 0 && (uintptr_t)argmax % 8 == 0) {
+    const long long t8 = total / 8;
+    if (dtype == 0)
+      hipLaunchKernelGGL(maxpool3s2_fwd8_kernel<float>, dim3(pool_grid(t8)), dim3(256), 0, s, (const float *)x, N, H,
+                         W, C, OH, OW, (float *)y, argmax);
+    else
+      hipLaunchKernelGGL(maxpool3s2_fwd8_kernel<__bf16>, dim3(pool_grid(t8)), dim3(256), 0, s, (const __bf16 *)x, N,
+                         H, W, C, OH, OW, (__bf16 *)y, argmax);
+    PC_CHECK_LAUNCH();
+    return PCOPS_OK;
+  }
+  if (dtype == 0)
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel<float>, dim3(pool_grid(total)), dim3(256), 0, s, (const float *)x, N, H,
+                       W, C, OH, OW, (float *)y, argmax);
+  else
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel<__bf16>, dim3(pool_grid(total)), dim3(256), 0, s, (const __bf16 *)x, N,
+                       H, W, C, OH, OW, (__bf16 *)y, argmax);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
+extern "C" int pcops_maxpool3s2_bwd(const void *gy, const unsigned char *argmax, int dtype, int N, int H, int W, int C,
+                                    void *gx, pcops_stream_t stream) {
+  if (N < 0 || H < 0 || W < 0 || C < 0 || (dtype != 0 && dtype != 1)) return PCOPS_ERR_INVALID;
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+  const long long total = (long long)N * H * W * C;
+  if (total == 0) return PCOPS_OK;
+  if (!gy || !argmax || !gx) return PCOPS_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  if (C % 8 == 0 && ((uintptr_t)gy | (uintptr_t)gx) % 16 == 0 && (uintptr_t)argmax % 8 == 0) {
+    const long long t8 = total / 8;
+    if (dtype == 0)
+      hipLaunchKernelGGL(maxpool3s2_bwd8_kernel<float>, dim3(pool_grid(t8)), dim3(256), 0, s, (const float *)gy,
+                         argmax, N, H, W, C, OH, OW, (float *)gx);
+    else
+      hipLaunchKernelGGL(maxpool3s2_bwd8_kernel<__bf16>, dim3(pool_grid(t8)), dim3(256), 0, s, (const __bf16 *)gy,
+                         argmax, N, H, W, C, OH, OW, (__bf16 *)gx);
+    PC_CHECK_LAUNCH();
+    return PCOPS_OK;
+  }
+  if (dtype == 0)
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel<float>, dim3(pool_grid(total)), dim3(256), 0, s, (const float *)gy,
+                       argmax, N, H, W, C, OH, OW, (float *)gx);
+  else
+    hipLaunchKernelGGL(maxpool3s2_bwd_kernel<__bf16>, dim3(pool_grid(total)), dim3(256), 0, s, (const __bf16 *)gy,
+                       argmax, N, H, W, C, OH, OW, (__bf16 *)gx);
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}

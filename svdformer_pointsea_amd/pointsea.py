@@ -32,7 +32,7 @@ from torch import nn
 from .attention import (PosEmbedding, SDG_Decoder_PointSea, _want_bf16, blend, block_sum, cross_attention,
                         self_attention, to_tokens)
 from .chamfer3D import chamfer_3DDist
-from ._lib import fork
+from ._lib import call, fork, lib, ptr, stream_of
 from .batchnorm import ACT_RELU, bn_act
 from .pointnet2_utils import furthest_point_sample, gather_operation
 from .svdformer import (MLP_CONV, BasicBlock, EdgeConv, FeatureExtractor, SinusoidalPositionalEmbedding, _lin,
@@ -74,8 +74,51 @@ class ResEncoder(nn.Module):
                 nn.init.constant_(m.bias, 0)
 
     def forward(self, input_view):
-        x = self.maxpool(bn_act(self.conv1(input_view), self.bn1, ACT_RELU))
+        x = maxpool3s2(self.maxpool, bn_act(self.conv1(input_view), self.bn1, ACT_RELU))
         return self.layer4(self.layer3(self.layer2(self.layer1(x))))
+
+
+class _MaxPool3s2(torch.autograd.Function):
+    """nn.MaxPool2d(3, 2, 1) on a channels_last activation on libpcops (pcops_maxpool3s2_fwd / _bwd):
+    torch's NHWC kernels ran this pool on a 3072-thread grid (104 + 149 us per PointSea step)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        OH, OW = (H + 1) // 2, (W + 1) // 2
+        y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        arg = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+        with torch.cuda.device(x.device):
+            call("maxpool3s2_fwd", lib().pcops_maxpool3s2_fwd, ptr(x), _POOL_DT[x.dtype], N, H, W, C, ptr(y), ptr(arg),
+                 stream_of(x))
+        ctx.save_for_backward(arg)
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        gx = torch.empty((N, C, H, W), dtype=gy.dtype, device=gy.device, memory_format=torch.channels_last)
+        with torch.cuda.device(gy.device):
+            call("maxpool3s2_bwd", lib().pcops_maxpool3s2_bwd, ptr(gy), ptr(arg), _POOL_DT[gy.dtype], N, H, W, C,
+                 ptr(gx), stream_of(gy))
+        return gx
+
+
+_POOL_DT = {torch.float32: 0, torch.bfloat16: 1}
+_PCOPS_POOL = os.environ.get("PCOPS_POOL", "1") != "0"   # A/B switch
+
+
+def maxpool3s2(pool, x):
+    """pool(x) for the stem's nn.MaxPool2d(3, 2, 1): _MaxPool3s2 on channels_last CUDA fp32 / bf16."""
+    if (_PCOPS_POOL and x.is_cuda and x.dim() == 4 and x.dtype in _POOL_DT and x.shape[1] > 0
+            and x.is_contiguous(memory_format=torch.channels_last) and pool.kernel_size in (3, (3, 3))
+            and pool.stride in (2, (2, 2)) and pool.padding in (1, (1, 1)) and pool.dilation in (1, (1, 1))
+            and not pool.ceil_mode and not pool.return_indices):
+        return _MaxPool3s2.apply(x)
+    return pool(x)
 
 
 # ----------------------------------------------------------------- refinement

@@ -198,3 +198,38 @@ def test_seprate_point_cloud_counts_bitwise(dev, monkeypatch):
             out.append(D.seprate_point_cloud(gt, n, crop, generator=torch.Generator(device=dev).manual_seed(9)))
         (a, ca), (b, cb) = out
         assert torch.equal(a, b) and torch.equal(ca, cb), crop
+
+
+@pytest.mark.parametrize("shape,dtype,kind", [((6, 64, 112, 112), torch.bfloat16, "relu"),
+                                              ((3, 16, 9, 14), torch.float32, "ties"),
+                                              ((2, 24, 15, 8), torch.bfloat16, "nan"),
+                                              ((4, 8, 1, 5), torch.float32, "relu")])
+def test_stem_maxpool_matches_torch_bitwise(dev, shape, dtype, kind):
+    """The ResEncoder stem's nn.MaxPool2d(3, 2, 1) on libpcops (pcops_maxpool3s2_fwd / _bwd) against
+    torch's own NHWC kernels: output and input gradient bitwise equal -- ties (the first maximum
+    wins), overlapping windows (an element winning several windows sums their gradients in torch's
+    order), NaN inputs, odd and single-row images."""
+    from torch import nn
+
+    from svdformer_pointsea_amd import pointsea as PS
+
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(shape, generator=g)
+    if kind == "relu":
+        x = x.clamp_min(0)
+    elif kind == "ties":
+        x = torch.round(x * 2) / 2      # many exact ties inside windows
+    else:
+        x[:, :, ::3, ::4] = float("nan")
+    x = x.to(dev, dtype).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(shape[0], shape[1], (shape[2] + 1) // 2, (shape[3] + 1) // 2, generator=g)
+    gy = gy.to(dev, dtype).contiguous(memory_format=torch.channels_last)
+    pool = nn.MaxPool2d(3, 2, 1)
+    out = []
+    for fn in (lambda t: pool(t), lambda t: PS.maxpool3s2(pool, t)):
+        xx = x.clone().requires_grad_(True)
+        y = fn(xx)
+        y.backward(gy)
+        out.append((y.detach(), xx.grad))
+    torch.testing.assert_close(out[1][0], out[0][0], rtol=0, atol=0, equal_nan=True)
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=0, atol=0, equal_nan=True)
