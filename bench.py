@@ -15,16 +15,18 @@ libpcops.so (hand-written gfx950 HIP); dense layers are torch (MIOpen /
 hipBLASLt).  N>1: one process per GPU, batch-partitioned (weak scaling),
 gradients all-reduced over RCCL by DDP -- the only data-path collective.
 
-Rank 0 prints ONE JSON line (the driver's contract) with, in addition:
-  roofline      -- dominant kernel: algorithmic FLOP (or bytes) per launch
-                   / mean launch duration, HIP events on the launch stream
-                   over the timed steps (DESIGN.md "Measurement");
+Rank 0 prints ONE JSON line (the driver's contract, kept under 8 KB: `compact`) with, in addition:
+  roofline      -- the dominant libpcops op (the attention core, all passes): algorithmic FLOP per
+                   launch / mean launch duration, HIP events on the launch stream (DESIGN.md 4);
   cpu_baseline  -- the same train step on the host CPU for a bounded sample
                    (oracle/cpu_path.py: torch CPU + the C restatement of the
                    point ops), rank 0 at N=1 only;
-  kernels       -- every libpcops call's launches / mean ms / roofline frac;
-  composite_fps_knn_chamfer -- sum of roofline times / sum of measured
-                   times for the FPS + kNN + Chamfer launches.
+  kernels       -- the 10 largest libpcops call groups: launches / ms per step / frac;
+  composite_fps_knn_chamfer -- sum of roofline times / sum of measured times for the FPS + kNN +
+                   Chamfer launches on the reference's work model; composite_hw the same
+                   on executed work (FPS on the VALU, the culled Chamfer's visited pairs).
+The full per-kernel tables of every leg go to profiles/bench_detail_<time>.json (--detail-json)
+and to stderr.
 """
 import argparse
 import json
@@ -87,6 +89,12 @@ def parse():
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r5_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
+    ap.add_argument("--pmc-valu-json", default=os.path.join(ROOT, "profiles", "r6_pmc_valu.json"),
+                    help="VALU-busy counters per kernel (tools/pmc_valu.py) -> north_star_kernels.*.pmc_valu_busy")
+    ap.add_argument("--visited-json", default=os.path.join(ROOT, "profiles", "r6_chamfer_visited.json"),
+                    help="pairs the culled Chamfer evaluates per launch shape (tools/chamfer_visited.py) -> hw_frac")
+    ap.add_argument("--detail-json", default=None,
+                    help="where the full per-kernel tables go (default profiles/bench_detail_<time>.json)")
     return ap.parse_args()
 
 
@@ -189,9 +197,10 @@ def kernel_work(name, a):
     if name == "furthest_point_sampling":
         B, N, M = a[1], a[2], a[3]
         return 16.0 * B * N * M, "GB/s", HBM_PEAK, "hbm"
-    if name == "chamfer_3D.forward":  # all-pairs equivalent (the culled search evaluates a fraction of them)
+    if name == "chamfer_3D.forward":  # over the pairs evaluated: the culled search visits a fraction of them
         B, N, M = a[2], a[3], a[4]
-        return 8.0 * 2 * B * N * M, "TFLOP/s", VALU_F32_PEAK, "valu"
+        f = (kernel_table.visited or {}).get(f"{N}x{M}", 1.0)
+        return 8.0 * 2 * B * N * M * f, "TFLOP/s", VALU_F32_PEAK, "valu"
     if name == "knn":
         B, S, N, C = a[2], a[3], a[4], a[5]
         return (2.0 * C + 2) * B * S * N, "TFLOP/s", VALU_F32_PEAK, "valu"
@@ -284,6 +293,29 @@ def kernel_work(name, a):
     return None
 
 
+def hw_work(name, a, visited=None):
+    """(work, unit, peak, bound) on the work the kernel really executes, where that differs from
+    kernel_work's reference model:
+      FPS      8 FLOP per point-iteration (3 sub, mul, 2 fma of the reference's distance) on the
+               VALU: the cloud stays in registers, so the 16-B/point-iteration HBM sweep of the
+               reference's kernel (sampling_gpu.cu:69-173) never happens -- a hardware frac of the
+               WHOLE chip, though one cloud occupies one CU;
+      Chamfer  8 FLOP per pair over the pairs the culled search actually evaluates (the visited
+               fraction per launch shape from a counting build, tools/chamfer_visited.py), the
+               all-pairs kernels over all pairs."""
+    if name == "furthest_point_sampling":
+        B, N, M = a[1], a[2], a[3]
+        return 8.0 * B * N * M, "TFLOP/s", VALU_F32_PEAK, "valu"
+    if name == "chamfer_3D.forward":
+        B, N, M = a[2], a[3], a[4]
+        f = (visited or {}).get(f"{N}x{M}")
+        if f is None:
+            f = 1.0 if N * M < (1 << 24) else None   # below 2^24 pairs the all-pairs screens run
+        return (None if f is None else 8.0 * 2 * B * N * M * f), "TFLOP/s", VALU_F32_PEAK, "valu"
+    w = kernel_work(name, a)
+    return w if w is None or w[3] != "hbm" else None
+
+
 # libpcops call -> the HIP kernel symbol(s) it launches (for the PMC lookup)
 _SYMBOLS = {"attention forward": "attn_fwd2_kernel", "attention bwd dq": "attn_dq2_kernel",
             "attention bwd": "attn_(delta2|dkv3|dqs)_kernel",
@@ -343,26 +375,71 @@ def kernel_table(spans):
             if name in ATTN_ARGS:
                 i = _attn_b(name, args)
                 key = f"{name} [D={args[i + 4]}, {'bf16' if args[i + 6] == 1 else 'fp32'}]"
-            r = rows.setdefault(key, {"name": name, "launches": 0, "ms": 0.0, "work": 0.0})
+            r = rows.setdefault(key, {"name": name, "launches": 0, "ms": 0.0, "work": 0.0, "hw": 0.0})
             r["launches"] += 1
             r["ms"] += e0.elapsed_time(e1)
             w = kernel_work(name, args)
             if w is not None:
                 r["work"] += w[0]
                 r["unit"], r["peak"], r["bound"] = w[1], w[2], w[3]
+            if name == "chamfer_3D.forward":
+                r["allpairs"] = r.get("allpairs", 0.0) + 16.0 * args[2] * args[3] * args[4]
+            h = hw_work(name, args, kernel_table.visited)
+            if h is None or h[0] is None:
+                r["hw"] = None
+            elif r["hw"] is not None:
+                r["hw"] += h[0]
+                r["hw_unit"], r["hw_peak"] = h[1], h[2]
     for r in rows.values():
         if "peak" in r and r["ms"] > 0:
             rate = r["work"] / (r["ms"] * 1e-3)
             r["achieved"] = rate / (1e12 if r["unit"] == "TFLOP/s" else 1e9)
             r["frac"] = rate / r["peak"]
             r["roof_ms"] = r["work"] / r["peak"] * 1e3
+        if r.get("hw") and r["ms"] > 0 and "hw_peak" in r:
+            rate = r["hw"] / (r["ms"] * 1e-3)
+            r["hw_achieved"] = rate / (1e12 if r["hw_unit"] == "TFLOP/s" else 1e9)
+            r["hw_frac"] = rate / r["hw_peak"]
+            r["hw_roof_ms"] = r["hw"] / r["hw_peak"] * 1e3
     return rows
 
 
+kernel_table.visited = None   # "NxM" -> visited pair fraction of the culled Chamfer (tools/chamfer_visited.py)
+
+
+def _attn_pmc(pa):
+    """Time-weighted MFMA utilisation of the attention kernels from a tools/pmc_attn.py pass."""
+    if not pa or not os.path.exists(pa):
+        return None
+    tab = json.load(open(pa))
+    tw = sum(v["avg_us"] * v["launches"] for v in tab.values() if "mfma_util" in v)
+    if tw <= 0:
+        return None
+    return round(sum(v["mfma_util"] * v["avg_us"] * v["launches"] for v in tab.values() if "mfma_util" in v) / tw, 4)
+
+
+def _valu_pmc(path, name):
+    """VALU busy fraction of the kernels behind one call group, launch-time weighted, from a
+    tools/pmc_valu.py pass (SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES-style counters), or None."""
+    import re
+    if not path or not os.path.exists(path) or name not in _SYMBOLS:
+        return None
+    pat = _SYMBOLS[name]
+    pat = pat[0] if isinstance(pat, tuple) else pat
+    rows = [v for k, v in json.load(open(path)).items() if re.search(pat, k) and "valu_busy" in v]
+    tw = sum(v["avg_us"] * v["launches"] for v in rows)
+    return round(sum(v["valu_busy"] * v["avg_us"] * v["launches"] for v in rows) / tw, 4) if tw > 0 else None
+
+
 def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
-    """The line's kernel fields for one train leg: `roofline` (the dominant libpcops
-    call group), `fps_us_per_round`, `composite_fps_knn_chamfer` and the per-call
-    `kernels` table (HIP-event times per step, frac, PMC traffic ratio)."""
+    """The kernel fields of one train leg (the FULL set, written to the detail file; `compact`
+    cuts them for the driver's one-line JSON):
+      roofline   the dominant libpcops op by time.  Ops are families: the attention core's
+                 forward / dQ / dK-dV launches at every head dim are one op (the reference's one
+                 attention call), every other call group is its own;
+      fps_us_per_round, composite_fps_knn_chamfer (the reference-model composite),
+      composite_hw (the same three groups priced on executed work: FPS on the VALU, Chamfer on
+                 the visited pairs), north_star_kernels, attention, kernels (every call group)."""
     out = {}
 
     def pmc_row(k, r):
@@ -378,16 +455,35 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
     timed = {k: r for k, r in rows.items() if "frac" in r}
     if not timed:
         return out
+    att = [(k, r) for k, r in timed.items() if r["name"] in ATTN_ARGS and r["unit"] == "TFLOP/s"]
+    att_ms = sum(r["ms"] for _, r in att)
     dom_key = max(timed, key=lambda k: timed[k]["ms"])
-    d = timed[dom_key]
-    out["roofline"] = {"kernel": dom_key, "bound": d["bound"], "achieved": round(d["achieved"], 2),
-                       "peak": d["peak"] / (1e12 if d["unit"] == "TFLOP/s" else 1e9), "unit": d["unit"],
-                       "frac": round(d["frac"], 4),
-                       "traffic": pmc_traffic(pmc_json, dom_key, d["name"]),
-                       "traffic_source": os.path.relpath(pmc_json, ROOT) if pmc_json else None,
-                       "avg_launch_ms": round(d["ms"] / d["launches"], 4),
-                       **{k2: v for k2, v in pmc_row(dom_key, d).items() if k2 == "pmc_gbs"},
-                       "work_per_launch": d["work"] / d["launches"]}
+    pa = getattr(kernel_summary, "pmc_attn_json", None)
+    if att and att_ms >= timed[dom_key]["ms"]:
+        w = sum(r["work"] for _, r in att)
+        n = sum(r["launches"] for _, r in att)
+        peak = max(r["peak"] for _, r in att)
+        tr = [pmc_traffic(pmc_json, k, r["name"]) for k, r in att]
+        traffic = (sum(t * r["launches"] for t, (_, r) in zip(tr, att)) / n) if all(t is not None for t in tr) else None
+        big = max(att, key=lambda kr: kr[1]["ms"])
+        out["roofline"] = {"kernel": "attention core (fwd + dQ + dK/dV passes, every head dim; libpcops attn_*_kernel)",
+                           "bound": "mfma", "achieved": round(w / (att_ms * 1e-3) / 1e12, 2), "peak": peak / 1e12,
+                           "unit": "TFLOP/s", "frac": round(w / (att_ms * 1e-3) / peak, 4),
+                           "traffic": None if traffic is None else round(traffic),
+                           "traffic_source": os.path.relpath(pmc_json, ROOT) if pmc_json and traffic else None,
+                           "avg_launch_ms": round(att_ms / n, 4), "launches": n,
+                           "work_per_launch": w / n, "pmc_mfma_util": _attn_pmc(pa),
+                           "largest_call": {"kernel": big[0], "frac": round(big[1]["frac"], 4),
+                                            "avg_launch_ms": round(big[1]["ms"] / big[1]["launches"], 4)}}
+    else:
+        d = timed[dom_key]
+        out["roofline"] = {"kernel": dom_key, "bound": d["bound"], "achieved": round(d["achieved"], 2),
+                           "peak": d["peak"] / (1e12 if d["unit"] == "TFLOP/s" else 1e9), "unit": d["unit"],
+                           "frac": round(d["frac"], 4),
+                           "traffic": pmc_traffic(pmc_json, dom_key, d["name"]),
+                           "traffic_source": os.path.relpath(pmc_json, ROOT) if pmc_json else None,
+                           "avg_launch_ms": round(d["ms"] / d["launches"], 4),
+                           "work_per_launch": d["work"] / d["launches"]}
     # FPS is M-1 serially dependent rounds: its honest figure is time per round
     fps = {}
     for e0, e1, a in spans.get("furthest_point_sampling", []):
@@ -402,48 +498,117 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
         f[0] += 1
         f[1] += e0.elapsed_time(e1)
     out["fps_us_per_round"] = {k: round(v[1] * 1e3 / v[0] / max(1, v[2] - 1), 3) for k, v in fps.items()}
-    group = [r for r in timed.values() if r["name"] in ("furthest_point_sampling", "knn", "chamfer_3D.forward")]
+    names3 = ("furthest_point_sampling", "knn", "chamfer_3D.forward")
+    group = [r for r in timed.values() if r["name"] in names3]
     if group:
         out["composite_fps_knn_chamfer"] = round(sum(r["roof_ms"] for r in group) / sum(r["ms"] for r in group), 4)
+        if all(r.get("hw_roof_ms") is not None for r in group):
+            out["composite_hw"] = round(sum(r["hw_roof_ms"] for r in group) / sum(r["ms"] for r in group), 4)
 
-    # SURVEY 8(d)'s three north_star kernel groups side by side: the algorithmic model rate and frac
-    # next to the rocprof-measured HBM bandwidth (PMC bytes / launch time) -- FPS keeps its cloud on
-    # chip, so its measured GB/s is small by design; kNN and Chamfer are VALU-bound
+    # SURVEY 8(d)'s three north_star kernel groups side by side: the reference-model rate and frac
+    # (FPS: the reference kernel's 16-B/point-iteration HBM sweep; Chamfer: all pairs), the frac on
+    # executed work (hw_frac) and the rocprof counters (HBM bytes, VALU busy)
+    vj = getattr(kernel_summary, "pmc_valu_json", None)
     out["north_star_kernels"] = {}
-    for k in ("furthest_point_sampling", "knn", "chamfer_3D.forward"):
+    for k in names3:
         r = rows.get(k)
         if r is None or "frac" not in r:
             continue
-        out["north_star_kernels"][k] = {"ms_per_step": round(r["ms"] / span_steps, 4),
-                                        "model_achieved": round(r["achieved"], 2), "model_unit": r["unit"],
-                                        "model_frac": round(r["frac"], 4), **pmc_row(k, r)}
+        row = {"ms_per_step": round(r["ms"] / span_steps, 4), "model_achieved": round(r["achieved"], 2),
+               "model_unit": r["unit"], "model_frac": round(r["frac"], 4)}
+        if r.get("hw_frac") is not None:
+            row.update(hw_achieved=round(r["hw_achieved"], 2), hw_unit=r["hw_unit"], hw_frac=round(r["hw_frac"], 4))
+        if k == "chamfer_3D.forward":
+            # the reference's all-pairs work at this speed (a rate, not a fraction of any roof), and
+            # whether every culled shape had a visited-pair count (else those launches are priced all-pairs)
+            row["allpairs_equiv_tflops"] = round(r.get("allpairs", 0.0) / (r["ms"] * 1e-3) / 1e12, 2)
+            row["pricing"] = "visited pairs" if r.get("hw") is not None else "all pairs (no visited count)"
+        vb = _valu_pmc(vj, k)
+        if vb is not None:
+            row["pmc_valu_busy"] = vb
+        row.update({k2: v for k2, v in pmc_row(k, r).items() if k2 != "pmc_bytes_per_launch"})
+        out["north_star_kernels"][k] = row
 
     # attention as ONE figure: credited FLOPs of every attention call / their summed launch time,
     # and the time-weighted MFMA utilisation of the attention kernels from a rocprofv3 --pmc pass
     # (tools/pmc_attn.py: SQ_VALU_MFMA_BUSY_CYCLES / (cycles x SIMDs))
-    att = [r for r in timed.values() if r["name"] in ATTN_ARGS and r["unit"] == "TFLOP/s"]
     if att:
-        w, ms = sum(r["work"] for r in att), sum(r["ms"] for r in att)
-        peak = max(r["peak"] for r in att)
-        agg = {"ms_per_step": round(ms / span_steps, 4), "achieved_tflops": round(w / (ms * 1e-3) / 1e12, 2),
-               "peak_tflops": peak / 1e12, "frac": round(w / (ms * 1e-3) / peak, 4)}
-        pa = getattr(kernel_summary, "pmc_attn_json", None)
-        if pa and os.path.exists(pa):
-            tab = json.load(open(pa))
-            tw = sum(v["avg_us"] * v["launches"] for v in tab.values() if "mfma_util" in v)
-            if tw > 0:
-                agg["pmc_mfma_util"] = round(sum(v["mfma_util"] * v["avg_us"] * v["launches"]
-                                                 for v in tab.values() if "mfma_util" in v) / tw, 4)
-                agg["pmc_source"] = os.path.relpath(pa, ROOT)
+        w = sum(r["work"] for _, r in att)
+        peak = max(r["peak"] for _, r in att)
+        agg = {"ms_per_step": round(att_ms / span_steps, 4), "achieved_tflops": round(w / (att_ms * 1e-3) / 1e12, 2),
+               "peak_tflops": peak / 1e12, "frac": round(w / (att_ms * 1e-3) / peak, 4)}
+        u = _attn_pmc(pa)
+        if u is not None:
+            agg["pmc_mfma_util"] = u
+            agg["pmc_source"] = os.path.relpath(pa, ROOT)
         out["attention"] = agg
 
     out["kernels"] = {k: {"launches_per_step": r["launches"] / span_steps,
                           "ms_per_step": round(r["ms"] / span_steps, 4),
                           "share": round(r["ms"] / span_steps / step_ms, 4),
                           **({"frac": round(r["frac"], 4), "bound": r["bound"]} if "frac" in r else {}),
+                          **({"hw_frac": round(r["hw_frac"], 4)} if r.get("hw_frac") is not None and
+                             r.get("hw_frac") != r.get("frac") else {}),
                           **pmc_row(k, r)}
                       for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["ms"])}
     return out
+
+
+LINE_LIMIT = 8192   # bytes: the driver stopped parsing the line at 26 KB (BENCH_r05 parsed: null)
+
+
+def _short_roof(r):
+    return {k: r[k] for k in ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic") if k in r}
+
+
+def _short_kernels(ks, top=10):
+    keep = ("launches_per_step", "ms_per_step", "frac", "hw_frac", "bound", "pmc_traffic_ratio")
+    return {k: {f: v[f] for f in keep if f in v} for k, v in list(ks.items())[:top]}
+
+
+def _short_leg(leg):
+    out = {k: leg[k] for k in ("batch", "dtype", "steps", "ms_per_step", "samples_per_s", "execution") if k in leg}
+    for k in ("composite_fps_knn_chamfer", "composite_hw"):
+        if k in leg:
+            out[k] = leg[k]
+    if "roofline" in leg:
+        out["roofline"] = _short_roof(leg["roofline"])
+    if "attention" in leg:
+        out["attention_frac"] = leg["attention"].get("frac")
+    if "kernels" in leg:
+        out["kernels_top3"] = {k: v.get("ms_per_step") for k, v in list(leg["kernels"].items())[:3]}
+    return out
+
+
+def compact(full, limit=LINE_LIMIT):
+    """The driver's one JSON line from the full result: the contract's fields, roofline,
+    cpu_baseline, the north_star groups, the attention aggregate, a 10-row kernel table and one
+    summary per extra leg.  Fields are dropped from the least important end until it fits."""
+    line = {k: v for k, v in full.items() if k not in ("kernels", "fp32_train_step", "pointsea_train_step",
+                                                      "fp32_forward_loss", "cpu_baseline", "emd", "roofline")}
+    line["roofline"] = full["roofline"] if "roofline" in full else None
+    if "kernels" in full:
+        line["kernels"] = _short_kernels(full["kernels"])
+    if "fp32_forward_loss" in full:
+        line["fp32_forward_loss"] = {k: full["fp32_forward_loss"][k] for k in ("batch", "ms_per_step", "samples_per_s")
+                                     if k in full["fp32_forward_loss"]}
+    for k in ("fp32_train_step", "pointsea_train_step"):
+        if k in full:
+            line[k] = _short_leg(full[k])
+    if "emd" in full:
+        line["emd"] = full["emd"]
+    if "cpu_baseline" in full:
+        cb = dict(full["cpu_baseline"])
+        cb.pop("step_s", None)
+        line["cpu_baseline"] = cb
+    for drop in ("kernels", "fps_us_per_round", "emd", "host_issue_ms_per_step", "kernel_timing"):
+        if len(json.dumps(line)) < limit:
+            break
+        if drop == "kernels" and "kernels" in line:
+            line["kernels"] = _short_kernels(full["kernels"], top=5)
+        else:
+            line.pop(drop, None)
+    return json.dumps(line)
 
 
 # ------------------------------------------------------------------ workloads
@@ -972,6 +1137,9 @@ def main():
     global _RESULT_FD
     args = parse()
     kernel_summary.pmc_attn_json = args.pmc_attn_json
+    kernel_summary.pmc_valu_json = args.pmc_valu_json
+    if args.visited_json and os.path.exists(args.visited_json):
+        kernel_table.visited = {k: v["visited_frac"] for k, v in json.load(open(args.visited_json)).items()}
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N`: one rank per GPU, started before anything touches the GPU
         sys.exit(self_launch(args))
@@ -1071,7 +1239,16 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             progress(f"timed {out['ms_per_step']:.2f} ms/step; CPU baseline")
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_steps)
-        line = json.dumps(out) + "\n"
+        # the full per-kernel tables go to a detail file and to stderr; stdout carries the compact line
+        detail = args.detail_json or os.path.join(ROOT, "profiles", f"bench_detail_{time.strftime('%Y%m%d_%H%M%S')}.json")
+        try:
+            os.makedirs(os.path.dirname(detail), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(out, f, indent=1)
+        except OSError as exc:
+            progress(f"detail file not written ({exc})")
+        print("[bench detail] " + json.dumps(out), file=sys.stderr, flush=True)
+        line = compact(out) + "\n"
         if _RESULT_FD is not None:
             sys.stdout.flush()
             os.write(_RESULT_FD, line.encode())

@@ -216,6 +216,104 @@ _SIDE = {}
 _TLS = threading.local()
 
 
+class CaptureTopology:
+    """Refuses, with a RuntimeError, a stream wait that would kill the process at
+    hipStreamEndCapture.
+
+    While capturing, torch's HIP runtime (7.0.51831) files every NON-ORIGIN stream
+    that waits on a captured event under the waited (producing) stream's list of
+    parallel capture streams and walks those lists recursively at end of capture.
+    A cycle in that filing -- a stream waiting on its own event, or a nested fork
+    joined back into the stream it forked from -- makes the walk recurse until the
+    stack overflows (a segfault inside capture_end, no Python traceback: the r5u
+    abort).  `wait(waiter, producer, origin)` is called before every wait the fork /
+    join / SharedFPS / fused-sum hand-offs issue; it keeps the filing graph of the
+    capture in progress (keyed by its capture id) and raises instead of issuing a
+    wait that closes a cycle.  Streams are identified by their integer handle, so
+    the check itself is plain host logic (tests/test_capture_guard.py)."""
+
+    def __init__(self):
+        self.cid = None
+        self.filed = {}   # producer handle -> set of waiter handles filed under it
+
+    def reset(self, cid=None):
+        self.cid, self.filed = cid, {}
+
+    def _reaches(self, a, b):
+        seen, todo = set(), [a]
+        while todo:
+            s = todo.pop()
+            if s == b:
+                return True
+            if s in seen:
+                continue
+            seen.add(s)
+            todo.extend(self.filed.get(s, ()))
+        return False
+
+    def wait(self, waiter, producer, origin, cid=None):
+        """Record (or refuse) `waiter` waiting on work of `producer` in capture `cid`."""
+        if cid != self.cid:
+            self.reset(cid)
+        if waiter == producer:
+            raise RuntimeError(
+                f"stream {waiter:#x} would wait on its own work while capturing a HIP graph: the runtime's "
+                "end-of-capture walk never returns on that (DESIGN.md 1.2); stream order already covers it")
+        if waiter == origin:
+            return   # the capture's origin stream is never filed
+        if self._reaches(waiter, producer):
+            raise RuntimeError(
+                f"stream {waiter:#x} waiting on stream {producer:#x} closes a cycle among the captured side "
+                "streams (each is already filed under the other): hipStreamEndCapture would never return "
+                "(DESIGN.md 1.2); fork from the outer origin (fork(..., base='outer')) or run inline")
+        self.filed.setdefault(producer, set()).add(waiter)
+
+
+_TOPO = CaptureTopology()
+_CAPINFO = []
+
+
+def _capture_id(stream):
+    """The id of the capture `stream` takes part in (hipStreamGetCaptureInfo of torch's own HIP
+    runtime), or None when that entry point cannot be reached."""
+    if not _CAPINFO:
+        fn = None
+        try:
+            h = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+            fn = h.hipStreamGetCaptureInfo
+            fn.restype = ctypes.c_int
+            fn.argtypes = [P, ctypes.POINTER(I), ctypes.POINTER(ULL)]
+        except (OSError, AttributeError):
+            fn = None
+        _CAPINFO.append(fn)
+    fn = _CAPINFO[0]
+    if fn is None:
+        return None
+    st, cid = I(0), ULL(0)
+    if fn(P(stream.cuda_stream), ctypes.byref(st), ctypes.byref(cid)) != 0 or st.value != 1:
+        return None
+    return cid.value
+
+
+def _origin(cur):
+    """The capture's origin stream: the outermost fork's base, else the stream current outside any fork."""
+    stack = getattr(_TLS, "mains", None)
+    return stack[0] if stack else cur
+
+
+def guarded_wait(waiter, producer, event=None, origin=None):
+    """waiter.wait_stream(producer) -- or waiter.wait_event(event) recorded on `producer` --
+    after the capture-topology check (a RuntimeError instead of a crash in capture_end).
+    `origin` defaults to the outermost fork's base, else the waiter itself (a top-level wait)."""
+    if torch.cuda.is_current_stream_capturing():
+        origin = origin if origin is not None else _origin(waiter)
+        _TOPO.wait(waiter.cuda_stream, producer.cuda_stream, origin.cuda_stream, _capture_id(waiter))
+    if event is not None:
+        waiter.wait_event(event)
+    else:
+        waiter.wait_stream(producer)
+
+
 def on_side_stream():
     """True inside a `fork` block on this thread (the block's ops run on a side stream)."""
     return getattr(_TLS, "side", 0) > 0
@@ -317,7 +415,7 @@ class fork:
 
     def __enter__(self):
         if self.on:
-            self.side.wait_stream(self.main)
+            guarded_wait(self.side, self.main, origin=_origin(self.main))
             for t in self.inputs:
                 t.record_stream(self.side)
             self._ctx = torch.cuda.stream(self.side)
@@ -338,7 +436,12 @@ class fork:
     def join(self, *tensors):
         if self.on:
             cur = torch.cuda.current_stream(self.side.device)
-            cur.wait_stream(self.side)
+            if cur == self.side:
+                # inside its own block: stream order already covers the tensors, and under capture the
+                # self-wait would hang hipStreamEndCapture -- a misuse, refused either way
+                raise RuntimeError("fork.join called on the fork's own side stream (inside its with-block); "
+                                   "join after the block")
+            guarded_wait(cur, self.side)
             for t in tensors:
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(cur)

@@ -176,7 +176,7 @@ def _take_sum(g):
     dsum, producer = ent
     cur = torch.cuda.current_stream(g.device)
     if producer != cur:
-        cur.wait_stream(producer)
+        _lib.guarded_wait(cur, producer)
     dsum.record_stream(cur)
     return dsum
 
@@ -394,11 +394,14 @@ class _RowSplit(Function):
     @staticmethod
     def forward(ctx, t, cuts):
         ctx.cuts = cuts
+        ctx.set_materialize_grads(False)   # a block without a gradient arrives as None: one zero fill, here
         return tuple(t[a:b] for a, b in zip(cuts[:-1], cuts[1:]))
 
     @staticmethod
     def backward(ctx, *gs):
-        ref = next(g for g in gs if g is not None)
+        ref = next((g for g in gs if g is not None), None)
+        if ref is None:
+            return None, None
         parts = [torch.zeros((b - a,) + tuple(ref.shape[1:]), dtype=ref.dtype, device=ref.device) if g is None else g
                  for g, a, b in zip(gs, ctx.cuts[:-1], ctx.cuts[1:])]
         return torch.cat(parts, 0), None

@@ -774,6 +774,28 @@ __global__ __launch_bounds__(kGThreads) void chamfer_grad_seg_kernel(
 #endif
 constexpr int kCullQB = 256, kCullTS = PCOPS_CULL_TS, kCullMaxTiles = 512, kCellBits = 4, kCells = 1 << (3 * kCellBits);
 
+// Visited-pair counting (a separate build, -DPCOPS_COUNT_PAIRS, libpcops_count.so; never the
+// product library): the (query, target) pairs the culled search evaluates, per pass --
+// [0] pass-1 screen lanes (a scanned tile costs every lane of the wave kCullTS pairs: lanes
+// whose own box test failed ride along), [1] pass-2 exact re-derivation rows, [2] reference
+// scans.  Each lane sums its own counts and adds them once at its end; read back by
+// pcops_debug_pair_counts (tools/chamfer_visited.py prices the bench's launches on them).
+#ifdef PCOPS_COUNT_PAIRS
+__device__ unsigned long long g_pairs[3];
+#define PAIRS_DECL unsigned long long np1 = 0, np2 = 0, np3 = 0
+#define PAIRS_ADD(v, n) (v += (unsigned long long)(n))
+#define PAIRS_FLUSH()                   \
+  do {                                  \
+    atomicAdd(&g_pairs[0], np1);        \
+    atomicAdd(&g_pairs[1], np2);        \
+    atomicAdd(&g_pairs[2], np3);        \
+  } while (0)
+#else
+#define PAIRS_DECL
+#define PAIRS_ADD(v, n) ((void)0)
+#define PAIRS_FLUSH() ((void)0)
+#endif
+
 __device__ __forceinline__ int cull_cell(float x, float y, float z, const float *g) {
   auto ax = [](float v, float lo, float sc) {
     const float t = fminf(fmaxf((v - lo) * sc, 0.f), float((1 << kCellBits) - 1));  // NaN -> 0
@@ -997,6 +1019,7 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
 #pragma unroll
   for (int c = 0; c < kSlots; ++c) cm[c] = INFINITY, cs[c] = -1;
   bool over = bad || !(an < INFINITY);
+  PAIRS_DECL;
   float mb = INFINITY;  // the wave's largest current bound (scalar)
   float m;
   int t;
@@ -1016,6 +1039,7 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
     const float pl = ((px * px + py * py) + pz * pz) * (1.f - 64.f * kU);
     const bool need = valid && (bad || !(pl > best) || pl <= 1e-30f);
     if (!__any(need)) continue;
+    if (valid) PAIRS_ADD(np1, kCullTS);
     if (ES) cur.w = (cur.x * cur.x + cur.y * cur.y) + cur.z * cur.z;  // |t|^2 (NaN padding stays NaN)
     // one wave: its LDS accesses complete in issue order, the wave barriers keep the compiler's
     __builtin_amdgcn_wave_barrier();
@@ -1072,6 +1096,7 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
   int bidx = INT_MAX;
   auto scan_tile = [&](int u) {   // the tile's sorted rows in batches of kRd loads issued together
     const int ke = min(NT, u * kCullTS + kCullTS);
+    PAIRS_ADD(np2, ke - u * kCullTS);
     for (int kb = u * kCullTS; kb < ke; kb += kRd) {
       float4 pr[kRd];
 #pragma unroll
@@ -1100,6 +1125,7 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
     }
   };
   if (nanst || !finite3(a.x, a.y, a.z)) {
+    PAIRS_ADD(np3, NT);
     ref_scan(Torig, NT, a.x, a.y, a.z, best, bidx);
   } else if (ES) {
     // pass 2, the exact (distance, original index) winner: over the candidate tiles, or -- on
@@ -1127,6 +1153,7 @@ __global__ __launch_bounds__(kCullQB) __attribute__((amdgpu_waves_per_eu(PCOPS_C
   const int oq = __float_as_int(a.w);
   dist[oq] = best;
   idx[oq] = bidx;
+  PAIRS_FLUSH();
 }
 
 size_t cull_ws_bytes(int B, int N, int M) {
@@ -1157,6 +1184,19 @@ bool cull_applies(int N, int M) {
 }
 
 }  // namespace
+
+#ifdef PCOPS_COUNT_PAIRS
+// counting build only (not in include/pcops.h): copy the three pair counters to host memory
+// `out` and zero them; synchronises the device
+extern "C" int pcops_debug_pair_counts(unsigned long long *out) {
+  if (hipDeviceSynchronize() != hipSuccess) return PCOPS_ERR_LAUNCH;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pairs), sizeof(unsigned long long) * 3) != hipSuccess)
+    return PCOPS_ERR_LAUNCH;
+  const unsigned long long zero[3] = {0, 0, 0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_pairs), zero, sizeof(zero)) != hipSuccess) return PCOPS_ERR_LAUNCH;
+  return PCOPS_OK;
+}
+#endif
 
 extern "C" int pcops_chamfer_forward(const float *xyz1, const float *xyz2, int B, int N, int M, float *dist1,
                                      float *dist2, int *idx1, int *idx2, pcops_stream_t stream) {

@@ -20,6 +20,7 @@ import os
 import torch
 from torch import nn
 
+from . import _lib
 from ._lib import Workspace, call, lib, ptr, require_float, stream_of
 from .pointnet2_utils import furthest_point_sample, furthest_point_sample_counts, gather_operation, grouping_operation
 
@@ -159,7 +160,7 @@ class SharedFPS:
             # capture a side stream waiting on its own event files itself in its own list of
             # parallel capture streams (HIP 7.0) -- the end-of-capture walk never returns (_lib.fork)
             if cur != self.stream:
-                cur.wait_event(self.event)
+                _lib.guarded_wait(cur, self.stream, event=self.event)
                 self.idx.record_stream(cur)
         return self.idx if m == self.idx.shape[1] else self.idx[:, :m].contiguous()
 

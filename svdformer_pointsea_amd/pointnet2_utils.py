@@ -110,8 +110,10 @@ class ThreeNN(Function):
         with torch.cuda.device(unknown.device):
             call("three_nn", lib().pcops_three_nn, ptr(unknown), ptr(known), B, n, m, ptr(dist2), ptr(idx),
                  stream_of(unknown))
-        ctx.mark_non_differentiable(dist2, idx)
-        return torch.sqrt(dist2), idx
+        dist = torch.sqrt(dist2)
+        # the RETURNED dist is the non-differentiable output (pointnet2_utils.py:124-127)
+        ctx.mark_non_differentiable(dist, idx)
+        return dist, idx
 
     @staticmethod
     @custom_bwd(device_type="cuda")

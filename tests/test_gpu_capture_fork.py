@@ -132,12 +132,14 @@ def test_captured_fills_every_replay(dev, what):
         torch.testing.assert_close(res, ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("model_name", ["pointsea", "svdformer"])
+@pytest.mark.parametrize("model_name", ["pointsea", "pointsea-nested-fps", "svdformer"])
 def test_model_step_capture_replays(dev, monkeypatch, model_name):
     """A whole model's forward + loss + backward at B = 2, captured and replayed THREE times (outputs
-    poisoned before each replay), against eager steps from the same state.  PointSea runs with the
-    local encoder's FPS on lane 3 nested in the lane-0 local-encoder fork (base="outer"); SVDFormer
-    with its image-branch and local-encoder side streams.  Not bitwise: the step is not bitwise
+    poisoned before each replay), against eager steps from the same state.  "pointsea" runs the
+    default path (one FPS of the partial cloud shared by the local encoder and the first SA module,
+    svdformer.SharedFPS); "pointsea-nested-fps" turns the sharing off so the local encoder's own FPS
+    runs on lane 3 nested in the lane-0 local-encoder fork (base="outer"); SVDFormer runs with its
+    image-branch and local-encoder side streams.  Not bitwise: the step is not bitwise
     reproducible EAGERLY (tools/capture_determinism.py: fp32 eager losses differ in the 7th digit run
     to run -- the dense GEMM / MIOpen conv libraries' reduction order; under bf16 autocast such
     differences flip FPS choices on the predicted clouds and move fine2 points by O(1)).  So this
@@ -151,8 +153,10 @@ def test_model_step_capture_replays(dev, monkeypatch, model_name):
     from svdformer_pointsea_amd.render import PCViews, PCViews_Real
 
     torch.manual_seed(1)
-    if model_name == "pointsea":
+    if model_name.startswith("pointsea"):
         monkeypatch.setattr(pointsea, "_LOCAL_FPS_FORK", True)
+        if model_name == "pointsea-nested-fps":
+            monkeypatch.setattr(svdformer, "_FPS_SHARE", False)
         model = pointsea.Model(pointsea.Config55).to(dev)
         partial, gt = synth_55(2, 6, dev)
         depth = PCViews_Real(TRANS=-pointsea.Config55.NETWORK.view_distance).get_img(partial)
@@ -197,7 +201,7 @@ def test_model_step_capture_replays(dev, monkeypatch, model_name):
         for (name, p), r, sp in zip(model.named_parameters(), ref_g, spread):
             if r is None:
                 assert p.grad is None
-            elif name.startswith("encoder.img_feature_extractor.") and model_name == "pointsea":
+            elif name.startswith("encoder.img_feature_extractor.") and model_name.startswith("pointsea"):
                 # PointSea's ResNet-18 runs on MIOpen (out of scope): its weight
                 # gradients in the captured step differ from eager by up to a few percent of their
                 # largest magnitude, on the graph's first launch by the most (the
@@ -212,3 +216,39 @@ def test_model_step_capture_replays(dev, monkeypatch, model_name):
                 # a BatchNorm: |g| ~ 1e-8)
                 err = float((p.grad - r).abs().max())
                 assert err <= 4 * float(sp) + 1e-4 * float(r.abs().max()) + 1e-7, (name, rep, err, float(sp))
+
+
+def test_capture_self_wait_raises(dev):
+    """A fork joined INSIDE its own block while capturing would make the side stream wait on its
+    own work; the HIP 7.0 runtime's end-of-capture walk never returns on that (the r5u abort,
+    DESIGN.md 1.2).  It must raise a RuntimeError in Python, and the capture must still close
+    (the proper join after the block) and replay correctly."""
+    from svdformer_pointsea_amd import _lib
+
+    x = torch.randn(1 << 16, device=dev)
+    ref = x * 2 + 1
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    caught = []
+    with torch.cuda.graph(g):
+        with _lib.fork(dev, inputs=(x,)) as br:
+            y = x * 2
+            try:
+                br.join(y)
+            except RuntimeError as exc:
+                caught.append(str(exc))
+            # a direct self-wait through the guard is refused the same way
+            s = torch.cuda.current_stream()
+            try:
+                _lib.guarded_wait(s, s)
+            except RuntimeError as exc:
+                caught.append(str(exc))
+        y = br.join(y) + 1
+    assert len(caught) == 2, caught
+    assert "own side stream" in caught[0] and "its own work" in caught[1]
+    y.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)

@@ -282,6 +282,18 @@ def test_three_nn_and_interpolate(dev):
                                atol=1e-5)
 
 
+def test_three_nn_dist_not_differentiable(dev):
+    """The reference marks the RETURNED dist (and idx) non-differentiable (pointnet2_utils.py:124-127):
+    with a grad-requiring input neither output requires grad."""
+    from svdformer_pointsea_amd.pointnet2_utils import three_nn
+
+    rng = np.random.default_rng(7)
+    u = T(rng.random((1, 64, 3)).astype(np.float32), dev).requires_grad_(True)
+    k = T(rng.random((1, 16, 3)).astype(np.float32), dev).requires_grad_(True)
+    dist, idx = three_nn(u, k)
+    assert not dist.requires_grad and not idx.requires_grad
+
+
 # ------------------------------------------------------------------ Chamfer
 @pytest.mark.parametrize("name", ["c1", "unit", "tiled"])
 def test_chamfer_golden(dev, name):

@@ -31,8 +31,8 @@ run_stage() {
              -k "${PYTEST_K:?set PYTEST_K}" > "$OUT/pytest_gpu_k.log" 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$OUT/smoke.log" 2>&1 ;;
     probe) timeout -k 10 60 ./tools/valu_probe > "$OUT/valu_probe.txt" 2>&1 ;;
-    bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
-    bench_ps) timeout -k 10 500 python bench.py --model pointsea > "$OUT/bench_pointsea.json" 2> "$OUT/bench_pointsea.err" ;;
+    bench) timeout -k 10 600 python bench.py --detail-json "$OUT/bench_detail.json" ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    bench_ps) timeout -k 10 500 python bench.py --model pointsea --detail-json "$OUT/bench_ps_detail.json" > "$OUT/bench_pointsea.json" 2> "$OUT/bench_pointsea.err" ;;
     bench_sa) PCOPS_CONV1X1=sa timeout -k 10 600 python bench.py --no-cpu-baseline --no-fp32-leg > "$OUT/bench_sa.json" \
              2> "$OUT/bench_sa.err" ;;
     bench_ps_sa) PCOPS_CONV1X1=sa timeout -k 10 500 python bench.py --model pointsea --no-cpu-baseline \
@@ -79,6 +79,18 @@ run_stage() {
         python tools/attn_bench.py 0 1 > "$OUT/pmc_attn.log" 2>&1 &&
       python tools/pmc_attn.py "$(find "$OUT/pmc_attn" -name '*counter_collection.csv' -print -quit)" \
         > "$OUT/pmc_attn_summary.json" ;;
+    pmc_valu)   # VALU counters of the north_star point kernels over the bench's own launches
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+        SQ_INSTS_SALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE \
+        --kernel-include-regex 'fps_|chamfer_|knn' --output-format csv -d "$OUT/pmc_valu" -o run -- \
+        python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-fp32-leg --no-extra-legs \
+        > /dev/null 2> "$OUT/pmc_valu.err" &&
+      python tools/pmc_valu.py "$(find "$OUT/pmc_valu" -name '*counter_collection.csv' -print -quit)" \
+        "$OUT/pmc_valu.json" > "$OUT/pmc_valu.txt" &&
+      find "$OUT/pmc_valu" -name '*.csv' -exec gzip -9 {} + ;;
+    visited)    # visited pairs of the culled Chamfer on the bench's launches (counting build)
+      PCOPS_LIB_PATH=svdformer_pointsea_amd/_lib/count/libpcops.so timeout -k 10 400 \
+        python tools/chamfer_visited.py "$OUT/chamfer_visited.json" > "$OUT/chamfer_visited.txt" 2>&1 ;;
     dist1) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
              --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg --no-extra-legs \
              > "$OUT/bench_dist1.json" 2> "$OUT/bench_dist1.err" ;;
