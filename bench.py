@@ -89,10 +89,16 @@ def parse():
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r5_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
+    ap.add_argument("--pmc-json-pointsea", default=os.path.join(ROOT, "profiles", "r6_pmc_traffic_pointsea.json"),
+                    help="the same HBM bytes table measured on the PointSea ShapeNet-55 step (its own shapes)")
     ap.add_argument("--pmc-valu-json", default=os.path.join(ROOT, "profiles", "r6_pmc_valu.json"),
                     help="VALU-busy counters per kernel (tools/pmc_valu.py) -> north_star_kernels.*.pmc_valu_busy")
     ap.add_argument("--visited-json", default=os.path.join(ROOT, "profiles", "r6_chamfer_visited.json"),
                     help="pairs the culled Chamfer evaluates per launch shape (tools/chamfer_visited.py) -> hw_frac")
+    ap.add_argument("--emd-pairs-json", default=os.path.join(ROOT, "profiles", "r6_emd_pairs.json"),
+                    help="auction bid pairs per shape (tools/emd_bench.py --count) -> emd.bid_gpairs_per_s")
+    ap.add_argument("--emd-pmc-json", default=os.path.join(ROOT, "profiles", "r6_pmc_emd.json"),
+                    help="VALU counters of the EMD kernels (tools/pmc_valu.py) -> emd.bid_pmc_valu_busy")
     ap.add_argument("--detail-json", default=None,
                     help="where the full per-kernel tables go (default profiles/bench_detail_<time>.json)")
     return ap.parse_args()
@@ -431,7 +437,7 @@ def _valu_pmc(path, name):
     return round(sum(v["valu_busy"] * v["avg_us"] * v["launches"] for v in rows) / tw, 4) if tw > 0 else None
 
 
-def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
+def kernel_summary(rows, spans, span_steps, step_ms, pmc_json, pmc_attn=None, pmc_valu=None):
     """The kernel fields of one train leg (the FULL set, written to the detail file; `compact`
     cuts them for the driver's one-line JSON):
       roofline   the dominant libpcops op by time.  Ops are families: the attention core's
@@ -458,7 +464,7 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
     att = [(k, r) for k, r in timed.items() if r["name"] in ATTN_ARGS and r["unit"] == "TFLOP/s"]
     att_ms = sum(r["ms"] for _, r in att)
     dom_key = max(timed, key=lambda k: timed[k]["ms"])
-    pa = getattr(kernel_summary, "pmc_attn_json", None)
+    pa = pmc_attn
     if att and att_ms >= timed[dom_key]["ms"]:
         w = sum(r["work"] for _, r in att)
         n = sum(r["launches"] for _, r in att)
@@ -508,7 +514,7 @@ def kernel_summary(rows, spans, span_steps, step_ms, pmc_json):
     # SURVEY 8(d)'s three north_star kernel groups side by side: the reference-model rate and frac
     # (FPS: the reference kernel's 16-B/point-iteration HBM sweep; Chamfer: all pairs), the frac on
     # executed work (hw_frac) and the rocprof counters (HBM bytes, VALU busy)
-    vj = getattr(kernel_summary, "pmc_valu_json", None)
+    vj = pmc_valu
     out["north_star_kernels"] = {}
     for k in names3:
         r = rows.get(k)
@@ -766,6 +772,48 @@ def fp32_forward_loss(wl, model, partial, gt, device, steps, use_graph, batch=16
     return {"config": "BASELINE configs[1]: SVDFormer forward + get_loss, PCN shapes, fp32", "batch": batch,
             "steps": steps, "ms_per_step": round(dt * 1e3, 3), "samples_per_s": round(batch / dt, 2),
             "execution": "hip_graph" if use_graph else "eager"}
+
+
+# ------------------------------------------------------------------ EMD (metrics/EMD, the auction)
+def emd_leg(device, pairs_json=None, pmc_json=None, B=32, n=2048, eps=0.005, iters=50):
+    """pcops_emd_forward / _backward at the reference's train settings (eps 0.005, 50 iterations:
+    metrics/EMD/README.md:7) on uniform clouds (emd_module.py:90-106 draws torch.rand), timed live
+    with HIP events (median of 3 after a warm-up); the bid pairs of the auction (unassigned bidders x
+    objects, per launch shape, from the counting build: tools/emd_bench.py --count) turn the forward
+    time into a pair rate, and a rocprofv3 pass over the bid kernel gives its VALU busy fraction."""
+    from svdformer_pointsea_amd.emd_module import emdModule
+
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x1 = torch.rand(B, n, 3, generator=g).to(device).requires_grad_(True)
+    x2 = torch.rand(B, n, 3, generator=g).to(device)
+    emd = emdModule()
+    fw, bw = [], []
+    for rep in range(4):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        x1.grad = None
+        e0.record()
+        dist, _ = emd(x1, x2, eps, iters)
+        e1.record()
+        dist.sum().backward()
+        e2.record()
+        torch.cuda.synchronize()
+        if rep:
+            fw.append(e0.elapsed_time(e1))
+            bw.append(e1.elapsed_time(e2))
+    out = {"shape": f"B{B} n{n}", "eps": eps, "iters": iters, "fwd_ms": round(sorted(fw)[1], 4),
+           "bwd_ms": round(sorted(bw)[1], 4)}
+    key = f"B{B} n{n}"
+    if pairs_json and os.path.exists(pairs_json):
+        c = json.load(open(pairs_json)).get(key)
+        if c:
+            out["bid_gpairs_per_s"] = round(c["active_pairs"] / (out["fwd_ms"] * 1e-3) / 1e9, 1)
+            out["active_pair_frac"] = round(c["active_pairs"] / c["all_pairs"], 4)
+    if pmc_json and os.path.exists(pmc_json):
+        rows = [v for k, v in json.load(open(pmc_json)).items() if "emd_bid_kernel" in k and "valu_busy" in v]
+        if rows:
+            tw = sum(v["avg_us"] * v["launches"] for v in rows)
+            out["bid_pmc_valu_busy"] = round(sum(v["valu_busy"] * v["avg_us"] * v["launches"] for v in rows) / tw, 4)
+    return out
 
 
 # ------------------------------------------------------------------ GEMM selection
@@ -1114,6 +1162,17 @@ def host_group():
     return _HOST_GROUP[0]
 
 
+def pmc_files(args, model, amp):
+    """The counter files measured on THIS workload's own launches (traffic, attention MFMA, VALU): a
+    table measured on another workload's shapes would misprice every ratio (round 5's PointSea
+    leg read the PCN step's LayerNorm bytes against PointSea's algorithmic bytes)."""
+    if not amp:
+        return None, None, None
+    if model == "pointsea":
+        return args.pmc_json_pointsea, None, None
+    return args.pmc_json, args.pmc_attn_json, args.pmc_valu_json
+
+
 def extra_leg(args, name, batch, amp, device, steps):
     """A second train-step figure beside the headline (rank 0, N = 1)."""
     wl = Workload(name)
@@ -1126,7 +1185,8 @@ def extra_leg(args, name, batch, amp, device, steps):
     if name == "pointsea" and amp:
         out["input_prefetch"] = not args.no_input_prefetch
     # the leg's own libpcops kernel table (HIP events of its eager timing steps)
-    out.update(kernel_summary(kernel_table(leg.spans), leg.spans, leg.span_steps, leg.ms_per_step, args.pmc_json))
+    out.update(kernel_summary(kernel_table(leg.spans), leg.spans, leg.span_steps, leg.ms_per_step,
+                              *pmc_files(args, name, amp)))
     del leg
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -1136,8 +1196,6 @@ def extra_leg(args, name, batch, amp, device, steps):
 def main():
     global _RESULT_FD
     args = parse()
-    kernel_summary.pmc_attn_json = args.pmc_attn_json
-    kernel_summary.pmc_valu_json = args.pmc_valu_json
     if args.visited_json and os.path.exists(args.visited_json):
         kernel_table.visited = {k: v["visited_frac"] for k, v in json.load(open(args.visited_json)).items()}
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1232,10 +1290,14 @@ def main():
                        "points_out": wl.n_out, "params": nparams,
                        "parallelism": f"dp{world}" if world > 1 else "single"},
         }
-        out.update(kernel_summary(rows, spans, span_steps, elapsed * 1e3 / args.steps, args.pmc_json))
+        out.update(kernel_summary(rows, spans, span_steps, elapsed * 1e3 / args.steps,
+                                  *pmc_files(args, args.model, amp)))
         if fp32_leg is not None:
             out["fp32_forward_loss"] = fp32_leg
         out.update(extra)
+        if world == 1 and not args.no_extra_legs:
+            progress("EMD at the reference's train settings")
+            out["emd"] = emd_leg(device, args.emd_pairs_json, args.emd_pmc_json)
         if world == 1 and not args.no_cpu_baseline:
             progress(f"timed {out['ms_per_step']:.2f} ms/step; CPU baseline")
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_steps)

@@ -52,6 +52,13 @@ __global__ void emd_init_kernel(int total, int *ass, State st) {
   st.max_idx[i] = INT_MAX;
 }
 
+// Bid-pair counting (the -DPCOPS_COUNT_PAIRS build only, tools/emd_bench.py): [0] (bidder, object)
+// pairs of the UNASSIGNED bidders -- the auction's work -- and [1] the lane-pairs the scan runs
+// (every lane of a block with at least one unassigned bidder scans along)
+#ifdef PCOPS_COUNT_PAIRS
+__device__ unsigned long long g_emd_pairs[2];
+#endif
+
 __global__ __launch_bounds__(kThreads) void emd_bid_kernel(const float *__restrict__ xyz1,
                                                            const float *__restrict__ xyz2, int n, float eps,
                                                            const int *__restrict__ ass, State st) {
@@ -61,6 +68,10 @@ __global__ __launch_bounds__(kThreads) void emd_bid_kernel(const float *__restri
   const size_t base = (size_t)b * n;
   const bool active = j < n && ass[base + j] == -1;
   if (!__syncthreads_or(active)) return;
+#ifdef PCOPS_COUNT_PAIRS
+  atomicAdd(&g_emd_pairs[0], active ? (unsigned long long)n : 0ull);
+  atomicAdd(&g_emd_pairs[1], (unsigned long long)n);
+#endif
   float x1 = 0.f, y1 = 0.f, z1 = 0.f;
   if (active) {
     x1 = xyz1[(base + j) * 3];
@@ -222,6 +233,18 @@ extern "C" int pcops_emd_forward(const float *xyz1, const float *xyz2, int B, in
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
+
+#ifdef PCOPS_COUNT_PAIRS
+// counting build only (not in include/pcops.h): the two bid-pair counters to `out`, then zeroed
+extern "C" int pcops_debug_emd_pair_counts(unsigned long long *out) {
+  if (hipDeviceSynchronize() != hipSuccess) return PCOPS_ERR_LAUNCH;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_emd_pairs), sizeof(unsigned long long) * 2) != hipSuccess)
+    return PCOPS_ERR_LAUNCH;
+  const unsigned long long zero[2] = {0, 0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_emd_pairs), zero, sizeof(zero)) != hipSuccess) return PCOPS_ERR_LAUNCH;
+  return PCOPS_OK;
+}
+#endif
 
 extern "C" int pcops_emd_backward(const float *xyz1, const float *xyz2, const float *graddist, const int *assignment,
                                   int B, int n, float *gradxyz1, pcops_stream_t stream) {

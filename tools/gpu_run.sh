@@ -62,16 +62,17 @@ run_stage() {
       find "$OUT/$1" -name '*kernel_trace.csv' -exec gzip -9 {} +
       [ $rc -eq 0 ] || tail -30 "$OUT/$1.err"
       return $rc ;;
-    pmc_traffic)
+    pmc_traffic|pmc_traffic_ps)
+      if [ "$1" = pmc_traffic_ps ]; then M="--model pointsea"; X=_ps; else M=""; X=""; fi
       timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
-        -d "$OUT/pmc_fetch" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
-        --no-fp32-leg --no-extra-legs > /dev/null 2> "$OUT/pmc_fetch.err" &&
+        -d "$OUT/pmc_fetch$X" -o run -- python bench.py $M --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+        --no-fp32-leg --no-extra-legs > /dev/null 2> "$OUT/pmc_fetch$X.err" &&
       timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PMC_RE" --output-format csv \
-        -d "$OUT/pmc_write" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
-        --no-fp32-leg --no-extra-legs > /dev/null 2> "$OUT/pmc_write.err" &&
-      python tools/pmc_traffic.py "$(find "$OUT/pmc_fetch" -name '*counter_collection.csv' -print -quit)" \
-        "$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)" "$OUT/pmc_traffic.json" &&
-      find "$OUT/pmc_fetch" "$OUT/pmc_write" -name '*.csv' -exec gzip -9 {} + ;;
+        -d "$OUT/pmc_write$X" -o run -- python bench.py $M --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+        --no-fp32-leg --no-extra-legs > /dev/null 2> "$OUT/pmc_write$X.err" &&
+      python tools/pmc_traffic.py "$(find "$OUT/pmc_fetch$X" -name '*counter_collection.csv' -print -quit)" \
+        "$(find "$OUT/pmc_write$X" -name '*counter_collection.csv' -print -quit)" "$OUT/pmc_traffic$X.json" &&
+      find "$OUT/pmc_fetch$X" "$OUT/pmc_write$X" -name '*.csv' -exec gzip -9 {} + ;;
     pmc_attn)
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA \
         SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
@@ -91,6 +92,24 @@ run_stage() {
     visited)    # visited pairs of the culled Chamfer on the bench's launches (counting build)
       PCOPS_LIB_PATH=svdformer_pointsea_amd/_lib/count/libpcops.so timeout -k 10 400 \
         python tools/chamfer_visited.py "$OUT/chamfer_visited.json" > "$OUT/chamfer_visited.txt" 2>&1 ;;
+    emd)        # EMD timing, bid-pair counts (counting build) and a VALU counter pass over the auction
+      timeout -k 10 300 python tools/emd_bench.py "$OUT/emd_bench.json" > "$OUT/emd_bench.txt" 2>&1 &&
+      PCOPS_LIB_PATH=svdformer_pointsea_amd/_lib/count/libpcops.so timeout -k 10 300 \
+        python tools/emd_bench.py --count "$OUT/emd_pairs.json" >> "$OUT/emd_bench.txt" 2>&1 &&
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+        SQ_INSTS_SALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE \
+        --kernel-include-regex 'emd_' --output-format csv -d "$OUT/pmc_emd" -o run -- \
+        python tools/emd_bench.py "$OUT/emd_bench_pmc.json" > /dev/null 2> "$OUT/pmc_emd.err" &&
+      python tools/pmc_valu.py "$(find "$OUT/pmc_emd" -name '*counter_collection.csv' -print -quit)" \
+        "$OUT/pmc_emd.json" > "$OUT/pmc_emd.txt" &&
+      find "$OUT/pmc_emd" -name '*.csv' -exec gzip -9 {} + ;;
+    grad_bisect)  # captured-step gradient report per env group in $BISECT ("A=0;B=0"; "X=1" = the default)
+      IFS=';' read -ra groups <<< "${BISECT:?set BISECT}"
+      for g in "${groups[@]}"; do
+        echo "== $g" >> "$OUT/grad_bisect.txt"
+        env $g timeout -k 10 240 python tools/capture_grad_report.py ${BISECT_MODEL:-pointsea} fp32 \
+          >> "$OUT/grad_bisect.txt" 2>&1 || return 1
+      done ;;
     dist1) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
              --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg --no-extra-legs \
              > "$OUT/bench_dist1.json" 2> "$OUT/bench_dist1.err" ;;
