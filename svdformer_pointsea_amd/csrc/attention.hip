@@ -448,6 +448,9 @@ constexpr int kKT = 64;  // keys per tile
 #define PCOPS_SCHED_DS 1
 #endif
 constexpr bool kSchedDs = PCOPS_SCHED_DS;  // 0: compiler's own LDS/MFMA order (A/B builds)
+#ifndef PCOPS_DQ_A
+#define PCOPS_DQ_A 2  // dQ pass (two-half form): LDS reads issued this many MFMAs ahead; 0 = plain chains (A/B)
+#endif
 #ifndef PCOPS_DEFER_LOG2
 #define PCOPS_DEFER_LOG2 8.f  // 0 = rescale on every max increase (A/B builds)
 #endif
@@ -641,11 +644,28 @@ struct Fwd2Cfg {
   typedef bf16x8 Regs[kCPT];
 };
 
-template <int D, int NW>
+// FAST: the full-tile form with one 32-bit offset per tensor (fewer VALU per load, but its
+// loop-invariant offsets cost registers): measured per kernel (profiles/r6_attn_lib_ab.txt) --
+// faster for the hd-64 forward and the dK/dV passes, slower for the hd-128 forward and dQ
+template <int D, int NW, bool FAST = false>
 __device__ __forceinline__ void fwd2_load(typename Fwd2Cfg<D, NW>::Regs &kr, typename Fwd2Cfg<D, NW>::Regs &vr,
                                           const __bf16 *Kb, long long ks, const __bf16 *Vb, long long vs, int k0,
                                           int Lk) {
   using C = Fwd2Cfg<D, NW>;
+  constexpr int RB = C::kThr % (D / 8) == 0 ? C::kThr / (D / 8) : 0;  // rows per pass of the block
+  if (FAST && RB && C::kChunks % C::kThr == 0 && k0 + kKT <= Lk) {
+    // a full tile: chunk t of the thread is row row0 + t RB at one column -- one unsigned 32-bit
+    // offset per tensor and a wave-uniform 64-bit row base per chunk (the per-chunk 64-bit multiply
+    // of the general form below cost ~10 VALU per load)
+    const unsigned tid = threadIdx.x, row0 = tid / (D / 8), col = (tid % (D / 8)) * 8;
+    const unsigned ok_ = row0 * (unsigned)ks + col, ov = row0 * (unsigned)vs + col;
+#pragma unroll
+    for (int t = 0; t < C::kCPT; ++t) {
+      kr[t] = *reinterpret_cast<const bf16x8 *>(Kb + (long long)(k0 + t * RB) * ks + ok_);
+      vr[t] = *reinterpret_cast<const bf16x8 *>(Vb + (long long)(k0 + t * RB) * vs + ov);
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < C::kCPT; ++t) {
     const int c = threadIdx.x + t * C::kThr;
@@ -656,10 +676,22 @@ __device__ __forceinline__ void fwd2_load(typename Fwd2Cfg<D, NW>::Regs &kr, typ
   }
 }
 
-template <int D, int NW>
+template <int D, int NW, bool FAST = false>
 __device__ __forceinline__ void fwd2_store(__bf16 *sk, __bf16 *sv, const typename Fwd2Cfg<D, NW>::Regs &kr,
                                            const typename Fwd2Cfg<D, NW>::Regs &vr) {
   using C = Fwd2Cfg<D, NW>;
+  constexpr int RB = C::kThr % (D / 8) == 0 ? C::kThr / (D / 8) : 0;
+  if constexpr (FAST && RB && RB % 16 == 0 && C::kChunks % C::kThr == 0) {
+    // Img<D>'s permutation reads row bits 0..3: rows row0 + t RB share it (immediate offsets)
+    const unsigned tid = threadIdx.x, row0 = tid / (D / 8), ch = tid % (D / 8);
+    const unsigned so = (unsigned)img_off<D>((int)row0, (int)ch);
+#pragma unroll
+    for (int t = 0; t < C::kCPT; ++t) {
+      *reinterpret_cast<bf16x8 *>(sk + so + t * RB * C::kKS) = kr[t];
+      *reinterpret_cast<bf16x8 *>(sv + so + t * RB * C::kVS) = vr[t];
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < C::kCPT; ++t) {
     const int c = threadIdx.x + t * C::kThr;
@@ -698,8 +730,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) Y[db] = f32x16{};
   typename C::Regs kr, vr;
-  fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
-  fwd2_store<D, NW>(sk, sv, kr, vr);
+  fwd2_load<D, NW, (D <= 64)>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
+  fwd2_store<D, NW, (D <= 64)>(sk, sv, kr, vr);
   lds_barrier();
   const int ntiles = (Lk + kKT - 1) / kKT;
   // one tile; EDGE: the last, partial tile (key masking), compiled separately
@@ -708,7 +740,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
     constexpr bool EDGE = decltype(edge_c)::value;
     const int cur = t & 1;
     const int k0 = t * kKT;
-    if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
+    if (t + 1 < ntiles) fwd2_load<D, NW, (D <= 64)>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
     f32x16 X0 = f32x16{}, X1 = f32x16{};
@@ -747,7 +779,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
     v_product<D>(Y, cv, X0);
     v_product<D>(Y, cv + 32 * C::kVS, X1);
     if constexpr (kSchedDs) sched_ds_mfma<D / 8, 2, (OCC >= 4 ? 1 : 2)>();
-    if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
+    if (t + 1 < ntiles) fwd2_store<D, NW, (D <= 64)>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   };
   const int nfull = Lk / kKT;
@@ -887,10 +919,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
       }
     } else {
       f32x16 S0 = f32x16{}, S1 = f32x16{}, G0 = f32x16{}, G1 = f32x16{};
+#if PCOPS_DQ_A > 0
+      // the two key halves' chains interleaved, each LDS read issued PCOPS_DQ_A MFMAs ahead
+      // (the plain chains waited lgkmcnt(0) before every MFMA: the read latency exposed 32 times
+      // a tile); per accumulator the MFMA order is k_product's, so dQ is bitwise unchanged
+      k_product2<D>(S0, ck, qf, S1, ck + 32 * C::kKS, qf);
+      sched_ds_mfma<D / 8, 1, PCOPS_DQ_A>();
+      k_product2<D>(G0, cv, gf, G1, cv + 32 * C::kVS, gf);
+      sched_ds_mfma<D / 8, 1, PCOPS_DQ_A>();
+#else
       k_product<D>(S0, ck, qf);
       k_product<D>(S1, ck + 32 * C::kKS, qf);
       k_product<D>(G0, cv, gf);
       k_product<D>(G1, cv + 32 * C::kVS, gf);
+#endif
   #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float p0 = exp2_ftz(__builtin_fmaf(S0[r], sl2, -lse2));
@@ -970,12 +1012,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
   }
   typename C::Regs qr, gr;
   float lr = INFINITY, dr = 0.f;
-  fwd2_load<D, NW>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, 0, Lq);
+  fwd2_load<D, NW, true>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, 0, Lq);
   if (threadIdx.x < kKT) {
     lr = threadIdx.x < Lq ? lse_b[threadIdx.x] * kLog2e : INFINITY;
     dr = threadIdx.x < Lq ? dl_b[threadIdx.x] : 0.f;
   }
-  fwd2_store<D, NW>(sq, sg, qr, gr);
+  fwd2_store<D, NW, true>(sq, sg, qr, gr);
   if (threadIdx.x < kKT) {
     slse[threadIdx.x] = lr;
     sdl[threadIdx.x] = dr;
@@ -986,7 +1028,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
     const int cur = t & 1;
     const int r0 = t * kKT;
     if (t + 1 < ntiles) {
-      fwd2_load<D, NW>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, r0 + kKT, Lq);
+      fwd2_load<D, NW, true>(qr, gr, Qb, st.q_srow, Gb, st.o_srow, r0 + kKT, Lq);
       if (threadIdx.x < kKT) {
         const int q = r0 + kKT + threadIdx.x;
         lr = q < Lq ? lse_b[q] * kLog2e : INFINITY;
@@ -1037,7 +1079,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC, OC
       }
     }
     if (t + 1 < ntiles) {
-      fwd2_store<D, NW>(sq + (cur ^ 1) * C::kKBuf, sg + (cur ^ 1) * C::kVBuf, qr, gr);
+      fwd2_store<D, NW, true>(sq + (cur ^ 1) * C::kKBuf, sg + (cur ^ 1) * C::kVBuf, qr, gr);
       if (threadIdx.x < kKT) {
         slse[(cur ^ 1) * kKT + threadIdx.x] = lr;
         sdl[(cur ^ 1) * kKT + threadIdx.x] = dr;
@@ -1299,9 +1341,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     asm volatile("" : "+v"(t));
     return t;
   };
+  // A thread's chunks c of a tile are rows row0 + c RB (RB = NW 64 / (D / 8) rows per pass) at one
+  // column: one unsigned 32-bit offset per tensor from the opaque thread id and a wave-uniform
+  // (scalar) step per chunk.  The signed form (row * (int)srow) cost ~250 VALU per tile: a signed
+  // division, a 64-bit sign extension and a 64-bit shift-add per chunk and tensor.
+  constexpr int RB = (NW * 64) % (D / 8) == 0 ? NW * 64 / (D / 8) : 0;
   auto load = [&](int t) {
     const int r0 = t * kKT;
-    if (r0 + kKT <= Lq) {
+    if (RB && r0 + kKT <= Lq) {
+      const __bf16 *qb = Qb + (long long)r0 * st.q_srow, *gb = Gb + (long long)r0 * st.o_srow;
+      const unsigned tid = (unsigned)tid_(), row0 = tid / (D / 8), col = (tid % (D / 8)) * 8;
+      const unsigned oq = row0 * (unsigned)st.q_srow + col, og = row0 * (unsigned)st.o_srow + col;
+#pragma unroll
+      for (int c = 0; c < kCPT; ++c) {
+        qr[c] = *reinterpret_cast<const bf16x8 *>(qb + (long long)(c * RB) * st.q_srow + oq);
+        gr[c] = *reinterpret_cast<const bf16x8 *>(gb + (long long)(c * RB) * st.o_srow + og);
+      }
+      lr = lse_b[r0 + l] * kLog2e;
+      dr = dl_b[r0 + l];
+    } else if (r0 + kKT <= Lq) {
       const __bf16 *qb = Qb + (long long)r0 * st.q_srow, *gb = Gb + (long long)r0 * st.o_srow;
       const int tid = tid_();
 #pragma unroll
@@ -1331,13 +1389,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   };
   // every wave writes the same 64 lse / delta values (no wave-dependent branch)
   auto store = [&](int slot) {
-    const int tid = tid_();
+    if constexpr (RB % 16 == 0 && RB) {
+      // Img<D>'s chunk permutation reads row bits 0..3 only: rows row0 + c RB share it, so every
+      // chunk of the thread lands at one base + c RB RS (an immediate offset)
+      const unsigned tid = (unsigned)tid_(), row0 = tid / (D / 8), ch = tid % (D / 8);
+      const unsigned so = (unsigned)img_off<D>((int)row0, (int)ch);
 #pragma unroll
-    for (int c = 0; c < kCPT; ++c) {
-      const int idx = tid + c * NW * 64;
-      const int row = idx / (D / 8), ch = idx % (D / 8);
-      *reinterpret_cast<bf16x8 *>(sq + slot * TB + img_off<D>(row, ch)) = qr[c];
-      *reinterpret_cast<bf16x8 *>(sg + slot * TB + img_off<D>(row, ch)) = gr[c];
+      for (int c = 0; c < kCPT; ++c) {
+        *reinterpret_cast<bf16x8 *>(sq + slot * TB + so + c * RB * RS) = qr[c];
+        *reinterpret_cast<bf16x8 *>(sg + slot * TB + so + c * RB * RS) = gr[c];
+      }
+    } else {
+      const int tid = tid_();
+#pragma unroll
+      for (int c = 0; c < kCPT; ++c) {
+        const int idx = tid + c * NW * 64;
+        const int row = idx / (D / 8), ch = idx % (D / 8);
+        *reinterpret_cast<bf16x8 *>(sq + slot * TB + img_off<D>(row, ch)) = qr[c];
+        *reinterpret_cast<bf16x8 *>(sg + slot * TB + img_off<D>(row, ch)) = gr[c];
+      }
     }
     slse[slot * kKT + l] = lr;
     sdl[slot * kKT + l] = dr;

@@ -10,14 +10,23 @@
 //   assign   winners replace the previous owner; price[k] += increment;
 //            in the last iteration every unassigned bidder takes its target.
 //
-// gfx950 layout: one lane per bidder (256-lane blocks, grid (n/256, B)); the
-// object cloud + prices stream through LDS in 1024-point float4 tiles that
-// every lane reads by broadcast, so the per-lane scan runs in ascending k
+// gfx950 layout: one lane per UNASSIGNED bidder.  After each assignment a
+// compaction pass lists every batch's unassigned bidders (the list order comes
+// from atomics, and does not matter: a bid depends on its bidder and the
+// iteration-start prices only, and the per-object maximum / lowest qualifying
+// bidder are order-independent atomics), and the bid launch runs 256-lane
+// blocks over that list; blocks past a batch's count exit at once.  Lanes no
+// longer idle beside assigned neighbours: after the first iterations ~90 % of
+// the bidders hold an object, and the one-lane-per-bidder grid had every block
+// scan all n objects while any of its 256 bidders bid (profiles/
+// r6_emd_pairs.json: lane-pairs = all pairs, active pairs 9.9 % at B 32 n 2048).
+// The object cloud + prices stream through LDS in 1024-point float4 tiles
+// that every lane reads by broadcast, so the per-lane scan runs in ascending k
 // exactly like the sequential rule (no cross-lane merge, no ties to break).
-// Blocks with no unassigned bidder exit before touching LDS.  The per-object
-// maximum is an atomicMax on an order-preserving integer key of the float
-// increment; the lowest qualifying bidder an atomicMin.  Per iteration:
-// bid, pick, assign = 3 launches; state lives in the caller's workspace.
+// The per-object maximum is an atomicMax on an order-preserving integer key of
+// the float increment; the lowest qualifying bidder an atomicMin.  Per
+// iteration: bid, pick, assign, compact = 4 launches; state lives in the
+// caller's workspace.
 #include "common.h"
 
 namespace {
@@ -40,9 +49,12 @@ struct State {
   float *bid_inc;     // (B,n)
   unsigned *max_key;  // (B,n) order_key(max increment on object), 0 = none
   int *max_idx;       // (B,n) lowest qualifying bidder, INT_MAX = none
+  int *list;          // (B,n) the unassigned bidders of the iteration (any order)
+  int *cnt;           // (B) their number
 };
 
-__global__ void emd_init_kernel(int total, int *ass, State st) {
+// every bidder unassigned: the first list is 0..n-1 in order
+__global__ void emd_init_kernel(int total, int n, int *ass, State st) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   ass[i] = -1;
@@ -50,6 +62,23 @@ __global__ void emd_init_kernel(int total, int *ass, State st) {
   st.price[i] = 0.f;
   st.max_key[i] = 0u;
   st.max_idx[i] = INT_MAX;
+  st.list[i] = i % n;
+  if (i % n == 0) st.cnt[i / n] = n;
+}
+
+// the unassigned bidders of batch b appended to its list (cnt was zeroed by the pick launch)
+__global__ void emd_compact_kernel(int n, const int *__restrict__ ass, State st) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool un = j < n && ass[(size_t)b * n + j] == -1;
+  // one atomic per wave: the wave's unassigned lanes take consecutive slots
+  const unsigned long long m = __ballot(un);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == (int)__builtin_ctzll(m)) base = atomicAdd(&st.cnt[b], (int)__popcll(m));
+  base = __shfl(base, (int)__builtin_ctzll(m), 64);
+  if (un) st.list[(size_t)b * n + base + (int)__popcll(m & ((1ull << lane) - 1))] = j;
 }
 
 // Bid-pair counting (the -DPCOPS_COUNT_PAIRS build only, tools/emd_bench.py): [0] (bidder, object)
@@ -59,18 +88,46 @@ __global__ void emd_init_kernel(int total, int *ass, State st) {
 __device__ unsigned long long g_emd_pairs[2];
 #endif
 
+// (best, better, index) of one bidder over a range of objects, merged in any order: the
+// sequential rule's result -- the largest value at its LOWEST k, and the largest of all the
+// other values (the second largest as a multiset) -- is order-free once equal bests keep the
+// lower k.  Float max / compares only: bitwise the ascending scan's result.
+__device__ __forceinline__ void bid_merge(float &best, float &better, int &bi, float ob, float obt, int oi) {
+  if (ob > best || (ob == best && oi >= 0 && (bi < 0 || oi < bi))) {
+    better = fmaxf(best, obt);
+    best = ob;
+    bi = oi;
+  } else {
+    better = fmaxf(better, ob);
+  }
+}
+
+// Block x of batch b takes bidders [x upb, (x+1) upb) of the batch's unassigned list,
+// upb = ceil(count / blocks), with T = the largest power of two <= min(64, 256 / upb) lanes per
+// bidder: lane t of a bidder scans objects [t s, (t+1) s) of every 1024-object LDS tile (s =
+// 1024 / T), in ascending order, and the T lanes' results are merged by a shuffle tree.  Early
+// iterations (every bidder unassigned) run T = 1: one lane per bidder over all objects; late
+// ones spread a few bidders over whole waves instead of leaving the chip idle behind them
+// (the reference splits bidders over threads the same way, emd_cuda.cu:95-175).
 __global__ __launch_bounds__(kThreads) void emd_bid_kernel(const float *__restrict__ xyz1,
                                                            const float *__restrict__ xyz2, int n, float eps,
                                                            const int *__restrict__ ass, State st) {
   __shared__ float4 tile[kTile];
   const int b = blockIdx.y;
-  const int j = blockIdx.x * kThreads + threadIdx.x;
+  const int nact = st.cnt[b];
+  const int upb = (nact + (int)gridDim.x - 1) / (int)gridDim.x;   // bidders per block
+  const int first = (int)blockIdx.x * upb;
+  if (upb == 0 || first >= nact) return;   // block-uniform: nothing of this batch's list here
+  int T = 1;
+  while (T < 64 && 2 * T * upb <= kThreads) T *= 2;
+  const int mine = min(upb, nact - first);   // bidders of this block
+  const int slot = threadIdx.x / T, t = threadIdx.x % T;
+  const bool active = slot < mine;
   const size_t base = (size_t)b * n;
-  const bool active = j < n && ass[base + j] == -1;
-  if (!__syncthreads_or(active)) return;
+  const int j = active ? st.list[base + first + slot] : 0;
 #ifdef PCOPS_COUNT_PAIRS
-  atomicAdd(&g_emd_pairs[0], active ? (unsigned long long)n : 0ull);
-  atomicAdd(&g_emd_pairs[1], (unsigned long long)n);
+  if (active && t == 0) atomicAdd(&g_emd_pairs[0], (unsigned long long)n);
+  if (threadIdx.x == 0) atomicAdd(&g_emd_pairs[1], (unsigned long long)kThreads * ((n + T - 1) / T));
 #endif
   float x1 = 0.f, y1 = 0.f, z1 = 0.f;
   if (active) {
@@ -82,22 +139,24 @@ __global__ __launch_bounds__(kThreads) void emd_bid_kernel(const float *__restri
   int best_i = -1;
   const float *p2 = xyz2 + base * 3;
   const float *price = st.price + base;
+  const int seg = kTile / T;
   for (int k0 = 0; k0 < n; k0 += kTile) {
     const int cnt = min(kTile, n - k0);
-    for (int t = threadIdx.x; t < cnt; t += kThreads) {
-      const int k = k0 + t;
-      tile[t] = make_float4(p2[3 * k], p2[3 * k + 1], p2[3 * k + 2], price[k]);
+    for (int q = threadIdx.x; q < cnt; q += kThreads) {
+      const int k = k0 + q;
+      tile[q] = make_float4(p2[3 * k], p2[3 * k + 1], p2[3 * k + 2], price[k]);
     }
     __syncthreads();
     if (active) {
-      for (int t = 0; t < cnt; ++t) {
-        const float4 q = tile[t];
-        const float d2 = sqd3(q.x - x1, q.y - y1, q.z - z1);
-        const float d = (float)((3.0 - (double)sqrtf(d2)) - (double)q.w);
+      const int e = min(cnt, (t + 1) * seg);
+      for (int q = t * seg; q < e; ++q) {
+        const float4 o = tile[q];
+        const float d2 = sqd3(o.x - x1, o.y - y1, o.z - z1);
+        const float d = (float)((3.0 - (double)sqrtf(d2)) - (double)o.w);
         if (d > best) {
           better = best;
           best = d;
-          best_i = k0 + t;
+          best_i = k0 + q;
         } else if (d > better) {
           better = d;
         }
@@ -105,7 +164,13 @@ __global__ __launch_bounds__(kThreads) void emd_bid_kernel(const float *__restri
     }
     __syncthreads();
   }
-  if (active) {
+  // the T lanes of a bidder (consecutive lanes of one wave): tree merge
+  for (int o = 1; o < T; o <<= 1) {
+    const float ob = __shfl_down(best, o, 64), obt = __shfl_down(better, o, 64);
+    const int oi = __shfl_down(best_i, o, 64);
+    if ((t & (2 * o - 1)) == 0) bid_merge(best, better, best_i, ob, obt, oi);
+  }
+  if (active && t == 0) {
     const float inc = best - better + eps;
     st.bid[base + j] = best_i;
     st.bid_inc[base + j] = inc;
@@ -116,6 +181,7 @@ __global__ __launch_bounds__(kThreads) void emd_bid_kernel(const float *__restri
 __global__ void emd_pick_kernel(int n, const int *__restrict__ ass, State st) {
   const int b = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j == 0) st.cnt[b] = 0;   // the bid launch has read the list: the compaction refills it
   if (j >= n) return;
   const size_t base = (size_t)b * n;
   if (ass[base + j] != -1) return;
@@ -198,6 +264,8 @@ State carve(void *ws, int B, int n) {
   st.bid_inc = (float *)(p + 12 * m);
   st.max_key = (unsigned *)(p + 16 * m);
   st.max_idx = (int *)(p + 20 * m);
+  st.list = (int *)(p + 24 * m);
+  st.cnt = (int *)(p + 28 * m);
   return st;
 }
 
@@ -205,7 +273,7 @@ State carve(void *ws, int B, int n) {
 
 extern "C" unsigned long long pcops_emd_workspace_bytes(int B, int n) {
   if (B <= 0 || n <= 0) return 0;
-  return 24ull * (unsigned long long)B * (unsigned long long)n;
+  return 28ull * (unsigned long long)B * (unsigned long long)n + 4ull * (unsigned long long)B;
 }
 
 extern "C" int pcops_emd_forward(const float *xyz1, const float *xyz2, int B, int n, float eps, int iters,
@@ -218,13 +286,14 @@ extern "C" int pcops_emd_forward(const float *xyz1, const float *xyz2, int B, in
   hipStream_t s = (hipStream_t)stream;
   const State st = carve(workspace, B, n);
   const int total = B * n;
-  hipLaunchKernelGGL(emd_init_kernel, dim3((total + 255) / 256), dim3(256), 0, s, total, assignment, st);
+  hipLaunchKernelGGL(emd_init_kernel, dim3((total + 255) / 256), dim3(256), 0, s, total, n, assignment, st);
   const dim3 g((n + kThreads - 1) / kThreads, B);
   for (int it = 0; it < iters; ++it) {
     hipLaunchKernelGGL(emd_bid_kernel, g, dim3(kThreads), 0, s, xyz1, xyz2, n, eps, assignment, st);
     if (it < iters - 1) {
       hipLaunchKernelGGL(emd_pick_kernel, g, dim3(kThreads), 0, s, n, assignment, st);
       hipLaunchKernelGGL(emd_assign_kernel, g, dim3(kThreads), 0, s, n, assignment, st);
+      hipLaunchKernelGGL(emd_compact_kernel, g, dim3(kThreads), 0, s, n, assignment, st);
     } else {
       hipLaunchKernelGGL(emd_assign_last_kernel, g, dim3(kThreads), 0, s, n, assignment, st);
     }

@@ -201,19 +201,22 @@ def test_model_step_capture_replays(dev, monkeypatch, model_name):
         for (name, p), r, sp in zip(model.named_parameters(), ref_g, spread):
             if r is None:
                 assert p.grad is None
-            elif name.startswith("encoder.img_feature_extractor.") and model_name.startswith("pointsea"):
-                # PointSea's ResNet-18 runs on MIOpen (out of scope): its weight
-                # gradients in the captured step differ from eager by up to a few percent of their
-                # largest magnitude, on the graph's first launch by the most (the
-                # ResEncoder captured alone matches eager within its run-to-run spread).  Held to
-                # 5 % here: a fill that does not happen is off by orders of magnitude
+            elif model_name == "pointsea-nested-fps" and name.startswith("encoder.img_feature_extractor."):
+                # the nested-FPS configuration (an A/B path, off by default: PCOPS_LOCAL_FPS_FORK)
+                # still shows round 5's first-replay deviation on the MIOpen ResNet (2.6e-4 of
+                # conv1.weight's largest magnitude on replay 1, r6 pytest log); held to 5 % there
                 err = float((p.grad - r).abs().max())
                 assert err <= 0.05 * float(r.abs().max()) + 1e-8, (name, rep, err)
             else:
-                # within 4x the eager run-to-run spread of that gradient (MIOpen's conv weight
-                # gradients vary by ~1e-3 run to run) plus 1e-4 of its largest magnitude; the 1e-7
-                # floor covers gradients that are rounding noise around 0 (a conv bias right before
-                # a BatchNorm: |g| ~ 1e-8)
+                # EVERY parameter on EVERY replay, the first included, within 4x the eager
+                # run-to-run spread of that gradient (MIOpen's conv weight gradients vary by ~1e-3
+                # run to run) plus 1e-4 of its largest magnitude; the 1e-7 floor covers gradients
+                # that are rounding noise around 0 (a conv bias right before a BatchNorm: |g| ~
+                # 1e-8).  Round 5 exempted PointSea's ResNet on the first replay (off by up to 3 %,
+                # profiles/r5_capture_grad_report_pointsea.txt); on the current tree it is within
+                # its eager spread on every replay (profiles/r6_capture_grad_report_pointsea.txt).
+                # The round-5 report predates the stem max-pool's move from torch's NHWC kernels
+                # to libpcops (1c518e3), the likely cause (not bisected further).
                 err = float((p.grad - r).abs().max())
                 assert err <= 4 * float(sp) + 1e-4 * float(r.abs().max()) + 1e-7, (name, rep, err, float(sp))
 

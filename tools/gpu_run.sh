@@ -110,6 +110,17 @@ run_stage() {
         env $g timeout -k 10 240 python tools/capture_grad_report.py ${BISECT_MODEL:-pointsea} fp32 \
           >> "$OUT/grad_bisect.txt" 2>&1 || return 1
       done ;;
+    attn_lib_ab)  # attention A/B of two builds of the library: $AB_BASE (a .so) vs the in-tree one,
+                  # attn_bench timings interleaved (base, new, base, new) + a bitwise comparison of outputs
+      for i in 1 2; do
+        for lib in "${AB_BASE:?set AB_BASE}" ${AB_MORE:-} svdformer_pointsea_amd/_lib/libpcops.so; do
+          PCOPS_LIB_PATH=$lib timeout -k 10 180 python tools/attn_bench.py ${ATTN_SHAPES:-0 1 2 3} >> "$OUT/attn_lib_ab.txt" 2>&1 || return 1
+        done
+      done
+      PCOPS_LIB_PATH=$AB_BASE timeout -k 10 300 python tools/attn_variant.py dump "$OUT/av_base.pt" > "$OUT/attn_lib_cmp.txt" 2>&1 &&
+      timeout -k 10 300 python tools/attn_variant.py dump "$OUT/av_new.pt" >> "$OUT/attn_lib_cmp.txt" 2>&1 &&
+      python tools/attn_variant.py cmp "$OUT/av_base.pt" "$OUT/av_new.pt" >> "$OUT/attn_lib_cmp.txt" 2>&1
+      rc=$?; rm -f "$OUT"/av_*.pt; return $rc ;;
     dist1) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
              --master-port 29611 bench.py --dist-selftest --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-leg --no-extra-legs \
              > "$OUT/bench_dist1.json" 2> "$OUT/bench_dist1.err" ;;
