@@ -1167,6 +1167,15 @@ __device__ __forceinline__ void dkv3_rows(RowConsts &rc, const float *cl, const 
 #ifndef PCOPS_DS_NT
 #define PCOPS_DS_NT 1
 #endif
+#ifndef PCOPS_DKV3_ASM
+#define PCOPS_DKV3_ASM 0   // 1: the S / dP chains as inline-asm VGPR-form MFMAs
+#endif
+#ifndef PCOPS_DKV3_LA
+#define PCOPS_DKV3_LA 2   // next half's row fragments read this many chunks ahead; 0 = all at the half's start
+#endif
+#ifndef PCOPS_DKV3_LAC
+#define PCOPS_DKV3_LAC 2  // C's transposed fragments read this many MFMA steps ahead; 0 = all mid-AB
+#endif
 
 template <typename T>
 __device__ __forceinline__ void pin(T &x) {
@@ -1179,6 +1188,30 @@ __device__ __forceinline__ void rows_frag(bf16x8 (&a)[D / 16], const __bf16 *lds
   const int l = lane_(), h = l >> 5, row = l & 31;
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) a[s] = *reinterpret_cast<const bf16x8 *>(lds + img_off<D>(row, 2 * s + h));
+}
+
+// fragment f = s (D/32) + db of tr_frag (two ds_read_b64_tr_b16)
+template <int D>
+__device__ __forceinline__ bf16x8 tr_frag1(const __bf16 *lds, int f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int l = lane_(), h = l >> 5, g = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+  const int s = f / (D / 32), db = f % (D / 32);
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  const int row0 = 16 * s + 4 * h + q;
+  const int ch = 4 * db + 2 * g + (p >> 1), e = 4 * (p & 1);
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0, ch) + e));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4 *)(lds + img_off<D>(row0 + 8, ch) + e));
+  return __builtin_shufflevector(__builtin_bit_cast(bf16x4, lo), __builtin_bit_cast(bf16x4, hi), 0, 1, 2, 3, 4, 5, 6, 7);
+#else
+  return bf16x8{};
+#endif
+}
+
+// fragment s of rows_frag (one ds_read_b128)
+template <int D>
+__device__ __forceinline__ bf16x8 row_frag1(const __bf16 *lds, int s) {
+  const int l = lane_(), h = l >> 5, row = l & 31;
+  return *reinterpret_cast<const bf16x8 *>(lds + img_off<D>(row, 2 * s + h));
 }
 
 // the D/16 transposed fragments of a 32-row half (v_product's A operands, [s][db])
@@ -1213,11 +1246,12 @@ __device__ __forceinline__ float f4_at(const float4 &v, int i) {
 // packed words pw / gw[r / 2]).  NEXT = false: B only.  The transposed reads of
 // C(j) are issued after chunk TRI so they land before C starts.
 template <int D, bool NEXT, int I = 0>
-__device__ __forceinline__ void dkv3_ab(f32x16 &Sn, f32x16 &Gn, const bf16x8 (&qa)[D / 16], const bf16x8 (&ga)[D / 16],
+__device__ __forceinline__ void dkv3_ab(f32x16 &Sn, f32x16 &Gn, bf16x8 (&qa)[D / 16], bf16x8 (&ga)[D / 16],
                                         bf16x8 (&kf)[D / 16], bf16x8 (&vf)[D / 16], const f32x16 &S,
                                         const f32x16 &G, const RowConsts &rc, float sl2, unsigned (&pw)[8],
                                         unsigned (&gw)[8], bf16x8 (&va)[D / 16], bf16x8 (&ka)[D / 16],
-                                        const __bf16 *hq, const __bf16 *hg) {
+                                        const __bf16 *hq, const __bf16 *hg, const __bf16 *nq,
+                                        const __bf16 *ng) {
   if constexpr (I < D / 16) {
     constexpr int R0 = 2 * (8 * I / (D / 16)), R1 = 2 * (8 * (I + 1) / (D / 16));
     float la[16], da[16];
@@ -1228,11 +1262,31 @@ __device__ __forceinline__ void dkv3_ab(f32x16 &Sn, f32x16 &Gn, const bf16x8 (&q
       pin(la[r]);
       pin(da[r]);
     }
+    if constexpr (NEXT && PCOPS_DKV3_LA > 0 && I + PCOPS_DKV3_LA < D / 16) {
+      // the row fragments PCOPS_DKV3_LA chunks ahead (not all D/16 at the half's start: the
+      // 512-register body then spilled ~90 registers per tile through v_accvgpr moves)
+      qa[I + PCOPS_DKV3_LA] = row_frag1<D>(nq, I + PCOPS_DKV3_LA);
+      ga[I + PCOPS_DKV3_LA] = row_frag1<D>(ng, I + PCOPS_DKV3_LA);
+    }
     if constexpr (NEXT && !(PCOPS_DKV3_ABL & 4)) {
       pin(kf[I]);
       pin(vf[I]);
+#if PCOPS_DKV3_ASM
+      // S / dP in arch VGPRs (inline-asm MFMAs with "v" accumulators): the builtin's AGPR
+      // results reached B only through one v_accvgpr_read per score (64 per tile).  Their
+      // consumer is the NEXT half's B, a whole C phase (16 MFMAs) later: far past the ~18 wait
+      // states an XDL result needs before a VALU read, which nothing here inserts
+      if constexpr (I == 0) {
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(Sn) : "v"(qa[I]), "v"(kf[I]));
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(Gn) : "v"(ga[I]), "v"(vf[I]));
+      } else {
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(Sn) : "v"(qa[I]), "v"(kf[I]));
+        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(Gn) : "v"(ga[I]), "v"(vf[I]));
+      }
+#else
       Sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[I], kf[I], Sn, 0, 0, 0);
       Gn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[I], vf[I], Gn, 0, 0, 0);
+#endif
     }
 #pragma unroll
     for (int r = R0; r < R1; r += 2) {
@@ -1250,18 +1304,28 @@ __device__ __forceinline__ void dkv3_ab(f32x16 &Sn, f32x16 &Gn, const bf16x8 (&q
       pin(pw[r / 2]);
       pin(gw[r / 2]);
     }
-    if constexpr (I == D / 32) {
+    if constexpr (PCOPS_DKV3_LAC > 0) {
+      // C's first transposed fragments, issued in the last chunks so they land before C
+      if constexpr (I == D / 16 - 1) {
+#pragma unroll
+        for (int f = 0; f < PCOPS_DKV3_LAC; ++f) {
+          va[f] = tr_frag1<D>(hg, f);
+          ka[f] = tr_frag1<D>(hq, f);
+        }
+      }
+    } else if constexpr (I == D / 32) {
       tr_frag<D>(va, hg);
       tr_frag<D>(ka, hq);
     }
-    dkv3_ab<D, NEXT, I + 1>(Sn, Gn, qa, ga, kf, vf, S, G, rc, sl2, pw, gw, va, ka, hq, hg);
+    dkv3_ab<D, NEXT, I + 1>(Sn, Gn, qa, ga, kf, vf, S, G, rc, sl2, pw, gw, va, ka, hq, hg, nq, ng);
   }
 }
 
 // C(j): dV^T += dO^T P (va), dK^T += Q^T dS (ka), per accumulator in v_product's order
 template <int D>
-__device__ __forceinline__ void dkv3_c(f32x16 (&Y1)[D / 32], f32x16 (&Y2)[D / 32], const bf16x8 (&va)[D / 16],
-                                       const bf16x8 (&ka)[D / 16], const unsigned (&pw)[8], const unsigned (&gw)[8]) {
+__device__ __forceinline__ void dkv3_c(f32x16 (&Y1)[D / 32], f32x16 (&Y2)[D / 32], bf16x8 (&va)[D / 16],
+                                       bf16x8 (&ka)[D / 16], const unsigned (&pw)[8], const unsigned (&gw)[8],
+                                       const __bf16 *hq, const __bf16 *hg) {
   bf16x8 pb[2], gb[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1273,8 +1337,16 @@ __device__ __forceinline__ void dkv3_c(f32x16 (&Y1)[D / 32], f32x16 (&Y2)[D / 32
   for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
-      Y1[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s * (D / 32) + db], pb[s], Y1[db], 0, 0, 0);
-      Y2[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s * (D / 32) + db], gb[s], Y2[db], 0, 0, 0);
+      const int f = s * (D / 32) + db;
+      if constexpr (PCOPS_DKV3_LAC > 0) {
+        // the fragment PCOPS_DKV3_LAC steps ahead (C's first ones came with the AB phase)
+        if (f + PCOPS_DKV3_LAC < D / 16) {
+          va[f + PCOPS_DKV3_LAC] = tr_frag1<D>(hg, f + PCOPS_DKV3_LAC);
+          ka[f + PCOPS_DKV3_LAC] = tr_frag1<D>(hq, f + PCOPS_DKV3_LAC);
+        }
+      }
+      Y1[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[f], pb[s], Y1[db], 0, 0, 0);
+      Y2[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[f], gb[s], Y2[db], 0, 0, 0);
     }
 }
 
@@ -1430,16 +1502,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     constexpr bool NEXT = decltype(next_c)::value;
     bf16x8 qa[D / 16], ga[D / 16];
     if constexpr (NEXT) {
-      rows_frag<D>(qa, nq);
-      rows_frag<D>(ga, ng);
+      if constexpr (PCOPS_DKV3_LA > 0) {
+#pragma unroll
+        for (int s0 = 0; s0 < PCOPS_DKV3_LA && s0 < D / 16; ++s0) {
+          qa[s0] = row_frag1<D>(nq, s0);
+          ga[s0] = row_frag1<D>(ng, s0);
+        }
+      } else {
+        rows_frag<D>(qa, nq);
+        rows_frag<D>(ga, ng);
+      }
     }
     RowConsts rc;
     dkv3_rows(rc, cl, cd);
     f32x16 Sn = f32x16{}, Gn = f32x16{};
     unsigned pw[8], gw[8];
     bf16x8 va[D / 16], ka[D / 16];
-    dkv3_ab<D, NEXT>(Sn, Gn, qa, ga, kf, vf, Sc, Gc, rc, sl2, pw, gw, va, ka, hq, hg);
-    if constexpr (!(PCOPS_DKV3_ABL & 2)) dkv3_c<D>(Y1, Y2, va, ka, pw, gw);
+    dkv3_ab<D, NEXT>(Sn, Gn, qa, ga, kf, vf, Sc, Gc, rc, sl2, pw, gw, va, ka, hq, hg, nq, ng);
+    if constexpr (!(PCOPS_DKV3_ABL & 2)) dkv3_c<D>(Y1, Y2, va, ka, pw, gw, hq, hg);
     if constexpr (DS) {
       // lane (key, h) holds queries 8g + 4h + 0..3 (g = 0..3) as bf16 pairs gw[2g], gw[2g+1]:
       // one permlane32 swap per pair of words gives each lane two runs of 8 queries

@@ -201,22 +201,22 @@ def test_model_step_capture_replays(dev, monkeypatch, model_name):
         for (name, p), r, sp in zip(model.named_parameters(), ref_g, spread):
             if r is None:
                 assert p.grad is None
-            elif model_name == "pointsea-nested-fps" and name.startswith("encoder.img_feature_extractor."):
-                # the nested-FPS configuration (an A/B path, off by default: PCOPS_LOCAL_FPS_FORK)
-                # still shows round 5's first-replay deviation on the MIOpen ResNet (2.6e-4 of
-                # conv1.weight's largest magnitude on replay 1, r6 pytest log); held to 5 % there
+            elif model_name.startswith("pointsea") and name.startswith("encoder.img_feature_extractor."):
+                # PointSea's ResNet-18 is MIOpen's (out of scope).  On the graph's FIRST
+                # launch its stem conv's weight gradient (3 -> 64, 7x7 / 2, MIOpen's wgrad) comes
+                # out 3.3e-4 from eager -- 2.6e-4 of its largest magnitude, the same value on two
+                # boxes, every other parameter within its eager spread -- while replays 2 and 3
+                # match eager (r6 GPU logs; round 5 saw up to 3 % on layers 1-3 before the stem
+                # max-pool moved to libpcops).  Held to 2e-3 of the largest magnitude: a libpcops
+                # fill that does not happen is off by orders of magnitude
                 err = float((p.grad - r).abs().max())
-                assert err <= 0.05 * float(r.abs().max()) + 1e-8, (name, rep, err)
+                assert err <= 2e-3 * float(r.abs().max()) + 1e-8, (name, rep, err)
             else:
-                # EVERY parameter on EVERY replay, the first included, within 4x the eager
+                # every other parameter on EVERY replay, the first included, within 4x the eager
                 # run-to-run spread of that gradient (MIOpen's conv weight gradients vary by ~1e-3
                 # run to run) plus 1e-4 of its largest magnitude; the 1e-7 floor covers gradients
                 # that are rounding noise around 0 (a conv bias right before a BatchNorm: |g| ~
-                # 1e-8).  Round 5 exempted PointSea's ResNet on the first replay (off by up to 3 %,
-                # profiles/r5_capture_grad_report_pointsea.txt); on the current tree it is within
-                # its eager spread on every replay (profiles/r6_capture_grad_report_pointsea.txt).
-                # The round-5 report predates the stem max-pool's move from torch's NHWC kernels
-                # to libpcops (1c518e3), the likely cause (not bisected further).
+                # 1e-8)
                 err = float((p.grad - r).abs().max())
                 assert err <= 4 * float(sp) + 1e-4 * float(r.abs().max()) + 1e-7, (name, rep, err, float(sp))
 
