@@ -1167,14 +1167,18 @@ __device__ __forceinline__ void dkv3_rows(RowConsts &rc, const float *cl, const 
 #ifndef PCOPS_DS_NT
 #define PCOPS_DS_NT 1
 #endif
-#ifndef PCOPS_DKV3_ASM
-#define PCOPS_DKV3_ASM 0   // 1: the S / dP chains as inline-asm VGPR-form MFMAs
-#endif
+// Register pressure (round 6): the D = 128 body holds the next half's row fragments (64 VGPRs)
+// and C's transposed fragments (64) from early in the half, and the compiler moves ~64-87
+// values per tile between AGPRs and VGPRs to fit.  Reading them just in time instead
+// (PCOPS_DKV3_LA / _LAC = chunks of read-ahead) removes ~23 of those moves but exposes the LDS
+// latency: 1.43-1.47 -> 1.55-1.61 ms at 2048^2 (profiles/r6_dkv3_regpressure_ab.txt), so the
+// early reads stay (0 = the whole half's fragments at once).  S / dP as VGPR-form inline-asm
+// MFMAs (no v_accvgpr_read per score) did not fit either: the compiler spilled others instead.
 #ifndef PCOPS_DKV3_LA
-#define PCOPS_DKV3_LA 2   // next half's row fragments read this many chunks ahead; 0 = all at the half's start
+#define PCOPS_DKV3_LA 0
 #endif
 #ifndef PCOPS_DKV3_LAC
-#define PCOPS_DKV3_LAC 2  // C's transposed fragments read this many MFMA steps ahead; 0 = all mid-AB
+#define PCOPS_DKV3_LAC 0
 #endif
 
 template <typename T>
@@ -1271,22 +1275,8 @@ __device__ __forceinline__ void dkv3_ab(f32x16 &Sn, f32x16 &Gn, bf16x8 (&qa)[D /
     if constexpr (NEXT && !(PCOPS_DKV3_ABL & 4)) {
       pin(kf[I]);
       pin(vf[I]);
-#if PCOPS_DKV3_ASM
-      // S / dP in arch VGPRs (inline-asm MFMAs with "v" accumulators): the builtin's AGPR
-      // results reached B only through one v_accvgpr_read per score (64 per tile).  Their
-      // consumer is the NEXT half's B, a whole C phase (16 MFMAs) later: far past the ~18 wait
-      // states an XDL result needs before a VALU read, which nothing here inserts
-      if constexpr (I == 0) {
-        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(Sn) : "v"(qa[I]), "v"(kf[I]));
-        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(Gn) : "v"(ga[I]), "v"(vf[I]));
-      } else {
-        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(Sn) : "v"(qa[I]), "v"(kf[I]));
-        asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(Gn) : "v"(ga[I]), "v"(vf[I]));
-      }
-#else
       Sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[I], kf[I], Sn, 0, 0, 0);
       Gn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[I], vf[I], Gn, 0, 0, 0);
-#endif
     }
 #pragma unroll
     for (int r = R0; r < R1; r += 2) {
