@@ -646,7 +646,8 @@ struct Fwd2Cfg {
 
 // FAST: the full-tile form with one 32-bit offset per tensor (fewer VALU per load, but its
 // loop-invariant offsets cost registers): measured per kernel (profiles/r6_attn_lib_ab.txt) --
-// faster for the hd-64 forward and the dK/dV passes, slower for the hd-128 forward and dQ
+// 1.5 % faster for the dK/dV pass (dkv2), slower for the hd-128 forward (+13 %) and dQ, a
+// wash for the hd-64 forward (which then reloaded two spilled offsets from scratch per tile)
 template <int D, int NW, bool FAST = false>
 __device__ __forceinline__ void fwd2_load(typename Fwd2Cfg<D, NW>::Regs &kr, typename Fwd2Cfg<D, NW>::Regs &vr,
                                           const __bf16 *Kb, long long ks, const __bf16 *Vb, long long vs, int k0,
@@ -730,8 +731,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
 #pragma unroll
   for (int db = 0; db < D / 32; ++db) Y[db] = f32x16{};
   typename C::Regs kr, vr;
-  fwd2_load<D, NW, (D <= 64)>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
-  fwd2_store<D, NW, (D <= 64)>(sk, sv, kr, vr);
+  fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, 0, Lk);
+  fwd2_store<D, NW>(sk, sv, kr, vr);
   lds_barrier();
   const int ntiles = (Lk + kKT - 1) / kKT;
   // one tile; EDGE: the last, partial tile (key masking), compiled separately
@@ -740,7 +741,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
     constexpr bool EDGE = decltype(edge_c)::value;
     const int cur = t & 1;
     const int k0 = t * kKT;
-    if (t + 1 < ntiles) fwd2_load<D, NW, (D <= 64)>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
+    if (t + 1 < ntiles) fwd2_load<D, NW>(kr, vr, Kb, st.k_srow, Vb, st.v_srow, k0 + kKT, Lk);
     const __bf16 *ck = sk + cur * C::kKBuf;
     const __bf16 *cv = sv + cur * C::kVBuf;
     f32x16 X0 = f32x16{}, X1 = f32x16{};
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(OCC))) 
     v_product<D>(Y, cv, X0);
     v_product<D>(Y, cv + 32 * C::kVS, X1);
     if constexpr (kSchedDs) sched_ds_mfma<D / 8, 2, (OCC >= 4 ? 1 : 2)>();
-    if (t + 1 < ntiles) fwd2_store<D, NW, (D <= 64)>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
+    if (t + 1 < ntiles) fwd2_store<D, NW>(sk + (cur ^ 1) * C::kKBuf, sv + (cur ^ 1) * C::kVBuf, kr, vr);
     lds_barrier();
   };
   const int nfull = Lk / kKT;
