@@ -306,6 +306,12 @@ int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, 
  * that feeds only GEMMs, models/model_utils.py:616).  16-byte aligned operands. */
 int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype, long long n,
               pcops_stream_t stream);
+/* pcops_add_rows: pcops_add over a contiguous (rows, C) a / b with out's rows ld_out elements apart: the
+ * refinement stage's two decoder outputs (SVDFormer.py:79-86, each `s + f` of a block feeding only conv_ps)
+ * written straight into the channel halves of `torch.cat([F_Q_, F_H_], 1)` (SVDFormer.py:86), which
+ * replaces the two sums plus the concatenation's copy.  C % 8 == 0, ld_out % 8 == 0, 16-byte aligned. */
+int pcops_add_rows(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype, long long rows,
+                   int C, long long ld_out, pcops_stream_t stream);
 /* pcops_add_posemb: out[b][m][h] = a[b][m][h] + E[b][h*N + m] for (B, N, H) token-major a / out,
  * where E (B, N*H) is SinusoidalPositionalEmbedding(cd) (models/model_utils.py:883-917:
  * E[b][n*H + 2i] = sin(cd[b][n] * div_term[i]), E[b][n*H + 2i + 1] = cos(...)) read through SDG's
@@ -371,6 +377,18 @@ int pcops_layernorm_bwd_bf16g(const void *dy_a, const void *dy16, const void *a,
                               int b_dtype, const float *gamma, const float *mean, const float *rstd, int rows, int C,
                               float *dx32, void *dx16, float *dgamma, float *dbeta, void *dsum, int dsum_src,
                               void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream);
+/* pcops_layernorm_bwd_ex: pcops_layernorm_bwd(_colsum / _bf16g) with dy = (dy + dy_x) + dy16:
+ *   dy (dy_dtype 0 fp32 / 1 bf16) the fp32 output's gradient with its rows ld_dy elements apart (a channel
+ *   slice of a wider gradient: the concatenation of SVDFormer.py:86 handed back without a contiguity copy);
+ *   dy_x (bf16, contiguous, optional, dy fp32 only) a second gradient of the same output, added to dy first --
+ *   the order autograd accumulates them in (the SDG query's positional add, `with_pos_embed(src1, pos)` of
+ *   models/model_utils.py:607, whose widening cast and accumulation this replaces); dy16 (bf16, optional) the
+ *   bf16 output's gradient.  dsum / dsum_src / workspace as pcops_layernorm_bwd_bf16g. */
+int pcops_layernorm_bwd_ex(const void *dy, int dy_dtype, long long ld_dy, const void *dy_x, const void *dy16,
+                           const void *a, int a_dtype, const void *b, int b_dtype, const float *gamma,
+                           const float *mean, const float *rstd, int rows, int C, float *dx32, void *dx16,
+                           float *dgamma, float *dbeta, void *dsum, int dsum_src, void *workspace,
+                           unsigned long long workspace_bytes, pcops_stream_t stream);
 /* pcops_gelu_bwd_colsum: du = dy * GELU'(u) (exact erf GELU, torch's GeluBackward expression in
  *   fp32) over a row-major (rows, C) matrix, dy / u / du all `dtype` (0 fp32, 1 bf16), C % 8 == 0;
  *   when dsum != NULL also dsum[c] = sum_r du[r][c] over du as stored (C values, fp32 accumulation,

@@ -68,6 +68,7 @@ _SIGS = {
     "pcops_transpose_add": (I, [P, I, P, I, P, I, P, I, I, I, I, P]),
     "pcops_add": (I, [P, I, P, I, P, I, LL, P]),
     "pcops_add_posemb": (I, [P, I, P, P, I, I, I, P, I, P]),
+    "pcops_add_rows": (I, [P, I, P, I, P, I, LL, I, LL, P]),
     "pcops_edge_group": (I, [P, P, I, I, I, I, P, I, P]),
     "pcops_edge_group_grad": (I, [P, I, P, I, I, I, I, P, P]),
     "pcops_max_k": (I, [P, I, LL, I, I, P, P, P]),
@@ -79,6 +80,7 @@ _SIGS = {
     "pcops_layernorm_bwd_colsum_workspace_bytes": (ULL, [I, I]),
     "pcops_layernorm_bwd_colsum": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, I, P, ULL, P]),
     "pcops_layernorm_bwd_bf16g": (I, [P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, I, P, ULL, P]),
+    "pcops_layernorm_bwd_ex": (I, [P, I, LL, P, P, P, I, P, I, P, P, P, I, I, P, P, P, P, P, I, P, ULL, P]),
     "pcops_adam_flat": (I, [P, P, P, LL, LL, P, P, P, P, D, P, D, D, D, D, I, P]),
     "pcops_blend_fwd": (I, [P, I, P, P, LL, P, I, P]),
     "pcops_blend_bwd": (I, [P, I, P, I, P, P, LL, P, P, P, P]),

@@ -565,10 +565,16 @@ class _LayerNorm(Function):
         C = a.shape[-1]
         rows = a.numel() // C
         ga16 = _take_g16(g32)   # y32's gradient as the bf16 block sum handed it down (_AddToBf16)
+        gx = _take_gx(ctx)      # y32's second gradient, bf16: the SDG query's positional add (_AddPosBf16)
         g16 = None if g16 is None else g16.contiguous().to(torch.bfloat16)
-        if ga16 is not None and g16 is None:
+        if ga16 is not None and (g16 is None or gx is not None):
             ga16, g32 = None, ga16.float()
+        if gx is not None and g32 is None:
+            gx, g32 = None, gx.float()
         g32 = None if (g32 is None or ga16 is not None) else g32.contiguous().float()
+        ld = _rows_ld(ga16) if ga16 is not None else C
+        if ld is None:
+            ga16, ld = ga16.contiguous(), C
         dtypes = {a.dtype} | ({b.dtype} if b is not None else set())
         dx32 = torch.empty(a.shape, dtype=torch.float32, device=a.device) if torch.float32 in dtypes else None
         dx16 = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device) if torch.bfloat16 in dtypes else None
@@ -577,17 +583,20 @@ class _LayerNorm(Function):
         src = None if ctx.sum_of is None else (a, b)[ctx.sum_of]
         need = (ctx.needs_input_grad[0], ctx.needs_input_grad[1])
         sflag = 2 if ctx.sum_dt == torch.bfloat16 else 0   # dsum_src bit 1: the sum stored bf16
-        if ga16 is not None:   # both upstream gradients bf16: widened inside the launch
+        if ga16 is not None or gx is not None:
+            # ga16: both upstream gradients bf16, widened inside the launch (its rows ld apart: a
+            # channel slice of the concatenation's gradient, _AddToBf16Cat); gx: added to g32 first
+            dy, dyt = (ga16, 1) if ga16 is not None else (g32, 0)
             dsum = (torch.empty(C, dtype=ctx.sum_dt, device=a.device) if (src is not None and need[ctx.sum_of])
                     else None)
             wsb = (lib().pcops_layernorm_bwd_colsum_workspace_bytes(rows, C) if dsum is not None
                    else lib().pcops_layernorm_bwd_workspace_bytes(rows, C))
             ws = _lib.Workspace.get(a.device, wsb)
             with torch.cuda.device(a.device):
-                call("layernorm_bwd", lib().pcops_layernorm_bwd_bf16g, ptr(ga16), ptr(g16), ptr(a), _dt(a), ptr(b),
-                     0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32), ptr(dx16),
-                     ptr(dw), ptr(db), ptr(dsum), (_DT[src.dtype] | sflag) if dsum is not None else 0, ptr(ws), wsb,
-                     stream_of(a))
+                call("layernorm_bwd", lib().pcops_layernorm_bwd_ex, ptr(dy), dyt, ld, ptr(gx), ptr(g16), ptr(a),
+                     _dt(a), ptr(b), 0 if b is None else _dt(b), ptr(w), ptr(mean), ptr(rstd), rows, C, ptr(dx32),
+                     ptr(dx16), ptr(dw), ptr(db), ptr(dsum), (_DT[src.dtype] | sflag) if dsum is not None else 0,
+                     ptr(ws), wsb, stream_of(a))
         elif src is not None and need[ctx.sum_of]:
             dsum = torch.empty(C, dtype=ctx.sum_dt, device=a.device)
             wsb = lib().pcops_layernorm_bwd_colsum_workspace_bytes(rows, C)
@@ -742,7 +751,8 @@ def _g16_handoff(g, shape):
     if nan is None:
         nan = _NAN_SCALAR[dev] = torch.full((), float("nan"), dtype=torch.float32, device=dev)
     fake = nan.expand(shape)
-    fake._pcops_g16 = g.contiguous()
+    # a channel slice of the concatenation's gradient (_AddToBf16Cat) is read in place
+    fake._pcops_g16 = g if (_LN_G16_LD and g.dtype == torch.bfloat16 and _rows_ld(g) is not None) else g.contiguous()
     return fake
 
 
@@ -753,6 +763,36 @@ def _take_g16(g):
     if h is not None:
         del g._pcops_g16
     return h
+
+
+def _rows_ld(t):
+    """Row stride (elements) of t viewed as (rows, C) with unit column stride and rows evenly
+    spaced -- a channel slice of a wider tensor -- or None."""
+    if t.stride(-1) != 1 or t.data_ptr() % 16:
+        return None
+    if t.dim() < 2:
+        return t.shape[-1]
+    ld = t.stride(-2)
+    span = ld
+    for d in range(t.dim() - 2, -1, -1):
+        if t.shape[d] > 1 and t.stride(d) != span:
+            return None
+        span *= t.shape[d]
+    return ld if (ld >= t.shape[-1] and ld % 8 == 0) else None
+
+
+def _take_gx(ctx):
+    """The bf16 gradient an _AddPosBf16 consumer of this LayerNorm's fp32 output left in the
+    node's mailbox (taken once, made safe on the consuming stream like _take_sum), or None."""
+    box = getattr(ctx, "gx_box", None)
+    if not box:
+        return None
+    g, producer = box.pop()
+    cur = torch.cuda.current_stream(g.device)
+    if producer != cur:
+        _lib.guarded_wait(cur, producer)
+    g.record_stream(cur)
+    return g
 
 
 class _AddToBf16(Function):
@@ -788,6 +828,66 @@ class _AddToBf16(Function):
         return ga, (ga if ctx.dts[1] == ctx.dts[0] else gb), None
 
 
+class _AddToBf16Cat(Function):
+    """torch.cat([bf16(s1 + f1), bf16(s2 + f2)], -1) written in place: each pair's sum stored by
+    pcops_add_rows into its channel half (the refinement stage's two decoder outputs feeding conv_ps,
+    SVDFormer.py:86) -- the values _AddToBf16 + cat produce, without the concatenation's copy.
+    Backward hands each pair its channel slice of the gradient in place: the Linear producing f
+    reads it with a leading dimension, the LayerNorm producing s (its only reader) through the
+    strided bf16 hand-off (_g16_handoff; pcops_layernorm_bwd_ex), where the slice was copied
+    contiguous before."""
+
+    @staticmethod
+    def forward(ctx, s1, f1, s2, f2):
+        C1, C2 = s1.shape[-1], s2.shape[-1]
+        out = torch.empty(s1.shape[:-1] + (C1 + C2,), dtype=torch.bfloat16, device=s1.device)
+        rows = out.numel() // (C1 + C2)
+        ctx.meta = []
+        off = 0
+        for a, b in ((s1, f1), (s2, f2)):
+            C = a.shape[-1]
+            a, b = a.contiguous(), b.contiguous()
+            with torch.cuda.device(a.device):
+                call("add_rows", lib().pcops_add_rows, ptr(a), _dt(a), ptr(b), _dt(b),
+                     out.data_ptr() + off * 2, 1, rows, C, C1 + C2, stream_of(a))
+            fn = a.grad_fn
+            handoff = (_LN_G16 and a.dtype == torch.float32 and fn is not None
+                       and type(fn).__name__ == "_LayerNormBackward" and a.output_nr == 0)
+            ctx.meta.append((off, C, a.dtype, b.dtype, handoff, a.shape))
+            off += C
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g if g.is_contiguous() else g.contiguous()
+        grads = []
+        for off, C, adt, bdt, handoff, shape in ctx.meta:
+            gh = g[..., off:off + C]
+            gb = gh.to(bdt)
+            if handoff and g.dtype == torch.bfloat16:
+                ga = _g16_handoff(gh, shape)
+            else:
+                ga = gh.to(adt)
+                if adt == bdt:
+                    gb = ga
+            grads += [ga, gb]
+        return tuple(grads)
+
+
+def block_sum_cat(p1, p2):
+    """torch.cat([block_sum(*p1, True), block_sum(*p2, True)], -1) for two (s, f) pairs of block
+    outputs read only by the GEMM the concatenation feeds (each s a block tail's LayerNorm output
+    nothing else reads): one bf16 buffer written in place under bf16 autocast."""
+    (s1, f1), (s2, f2) = p1, p2
+    if (_CAT_ROWS and _BLOCK_SUM16 and _PCOPS_ADD and _want_bf16() and s1.is_cuda
+            and s1.shape == f1.shape and s2.shape == f2.shape and s1.shape[:-1] == s2.shape[:-1]
+            and s1.shape[-1] % 8 == 0 and s2.shape[-1] % 8 == 0
+            and all(t.dtype in _DT for t in (s1, f1, s2, f2))):
+        return _AddToBf16Cat.apply(s1, f1, s2, f2)
+    a, b = block_sum(s1, f1, True), block_sum(s2, f2, True)
+    return torch.cat([a, b.to(a.dtype)], dim=-1)
+
+
 class PosEmbedding:
     """SDG's positional term, kept lazy: SinusoidalPositionalEmbedding(cd) (models/model_utils.py:
     883-917) read through the reference's raw .reshape(B, hidden, N).permute (SVDFormer.py:77-80),
@@ -817,10 +917,21 @@ class _AddPosBf16(Function):
             call("add_posemb", lib().pcops_add_posemb, ptr(s), _dt(s), ptr(cd), ptr(div), B, N, H, ptr(out), 1,
                  stream_of(s))
         ctx.sdt = s.dtype
+        # s is a LayerNorm's fp32 output that the block also reads elsewhere (the residual into
+        # norm12): instead of widening this gradient and letting autograd add it to the other one,
+        # hand it to that LayerNorm's backward, which adds it in the same order inside its launch
+        fn = s.grad_fn
+        ctx.box = None
+        if (_POS_GX and s.dtype == torch.float32 and fn is not None and type(fn).__name__ == "_LayerNormBackward"
+                and s.output_nr == 0 and getattr(fn, "gx_box", None) is None):
+            ctx.box = fn.gx_box = []
         return out
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.box is not None and g.dtype == torch.bfloat16 and g.is_contiguous() and not ctx.box:
+            ctx.box.append((g, torch.cuda.current_stream(g.device)))
+            return None, None, None
         return g.to(ctx.sdt), None, None
 
 
@@ -882,6 +993,9 @@ def block_sum(s, f, single_use=False):
 
 _BLOCK_SUM16 = os.environ.get("PCOPS_BLOCKSUM16", "1") != "0"   # A/B switch
 _PCOPS_POSEMB = os.environ.get("PCOPS_POSEMB", "1") != "0"          # A/B switch: fused add + positional embedding
+_POS_GX = os.environ.get("PCOPS_POS_GX", "1") != "0"   # A/B switch: positional add's gradient summed in the LN backward
+_CAT_ROWS = os.environ.get("PCOPS_CAT_ROWS", "1") != "0"   # A/B switch: decoder outputs written into their concatenation
+_LN_G16_LD = os.environ.get("PCOPS_LN_G16_LD", "1") != "0"   # A/B switch: strided bf16 hand-off read in place
 _FUSED_BIAS_SUM = os.environ.get("PCOPS_LN_BIASSUM", "1") != "0"   # A/B switch: LayerNorm-fused bias column sums
 _PCOPS_ADD = os.environ.get("PCOPS_ADD", "1") != "0"                 # A/B switch: pcops_add for the block sums
 _WGRAD_SPLITK = os.environ.get("PCOPS_WGRAD_SPLITK", "1") != "0"     # A/B switch: split-K weight gradients
@@ -975,9 +1089,12 @@ class SDG_Decoder(nn.Module):
         self.sa2 = self_attention(hidden_dim, channel * ratio, dropout=0.0, nhead=8)
 
     def forward_tokens(self, x_tok):
+        return block_sum(*self.forward_pair(x_tok), True)   # SDG feeds it to input_proj / conv_ps
+
+    def forward_pair(self, x_tok):
+        """The output as sa2's (residual, FFN) pair, summed by the consumer."""
         s, f = self.sa1.forward_tokens(x_tok)
-        s, f = self.sa2.forward_tokens(block_sum(s, f, True))   # sa2 starts with input_proj (a GEMM)
-        return block_sum(s, f, True)                             # SDG feeds it to input_proj / conv_ps
+        return self.sa2.forward_tokens(block_sum(s, f, True))   # sa2 starts with input_proj (a GEMM)
 
     def forward(self, input):
         s, f = self.sa1.forward_tokens(to_tokens(input))

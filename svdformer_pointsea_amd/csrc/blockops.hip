@@ -176,17 +176,21 @@ int ln_bwd_rpw(int rows) {
 }
 
 // CH: 8-element chunks per lane (1 for C <= 512, 2 for C <= 1024); AT / BT as
-// the forward; GM: which upstream gradients are present (1 = dy32, 2 = dy16,
-// 3 both; 7 = both, the first one bf16 too: the fp32 output's gradient as the bf16
-// block sum handed it down, widened here instead of by a separate cast pass); CS: also the column sums of dx (the bias gradient of the Linear
+// the forward; GM: which upstream gradients are present (bit 0 = dy32, bit 1 = dy16;
+// bit 2: the first one bf16 (the fp32 output's gradient as the bf16 block sum handed
+// it down, widened here instead of by a separate cast pass), its rows ldg elements
+// apart (a channel slice of the concatenation's gradient); bit 3: a second bf16
+// gradient of the fp32 output, gx (the SDG query's positional add), added to dy32
+// first -- autograd's accumulation of the two, then the sum with dy16 as before).
+// Instantiated: 1, 2, 3, 5, 7, 9, 11.  CS: also the column sums of dx (the bias gradient of the Linear
 // whose output is a or b) over the values as stored -- bf16-rounded when
 // sum16 -- as a third C-wide partial row.
 template <int CH, int AT, int BT, int GM, bool CS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4 : 3))) void ln_bwd_kernel(
-    const float *__restrict__ g32, const __bf16 *__restrict__ g16, const void *__restrict__ a,
-    const void *__restrict__ b, const float *__restrict__ gamma, const float *__restrict__ mean_in,
-    const float *__restrict__ rstd_in, int rows, int C, float *__restrict__ dx32, __bf16 *__restrict__ dx16, int rpw,
-    float *__restrict__ part, bool sum16) {
+    const float *__restrict__ g32, const __bf16 *__restrict__ g16, const __bf16 *__restrict__ gx, long long ldg,
+    const void *__restrict__ a, const void *__restrict__ b, const float *__restrict__ gamma,
+    const float *__restrict__ mean_in, const float *__restrict__ rstd_in, int rows, int C, float *__restrict__ dx32,
+    __bf16 *__restrict__ dx16, int rpw, float *__restrict__ part, bool sum16) {
   constexpr int NP = CS ? 3 : 2;     // partial rows per block: dgamma | dbeta (| dsum)
   extern __shared__ float ln_red[];  // [4][NP*C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -207,13 +211,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
     const float mean = mean_in[row], rstd = rstd_in[row];
     // all loads of the row first (clamped chunk index, no branches), then the
     // arithmetic; lanes past the row end carry dy = xh = 0
-    V8 xh[CH], dy[CH], t[CH], u[CH], v[CH];
+    V8 xh[CH], dy[CH], t[CH], u[CH], v[CH], q[(GM & 8) ? CH : 1];
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      const long long e = base + 8 * min(lane + 64 * i, nch - 1);
+      const int c8 = 8 * min(lane + 64 * i, nch - 1);
+      const long long e = base + c8;
       ld8c<AT>(xh[i], a, e);
       if constexpr (BT >= 0) ld8c<BT>(t[i], b, e);
-      if constexpr (GM & 1) ld8c<(GM & 4) ? 1 : 0>(u[i], g32, e);
+      if constexpr (GM & 1) ld8c<(GM & 4) ? 1 : 0>(u[i], g32, (long long)row * ldg + c8);
+      if constexpr (GM & 8) ld8c<1>(q[i], gx, e);
       if constexpr (GM & 2) ld8c<1>(v[i], g16, e);
     }
     float sg = 0.f, sgx = 0.f;
@@ -225,12 +231,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
         float x = xh[i].v[k];
         if constexpr (BT >= 0) x += t[i].v[k];
         float d;
-        if constexpr ((GM & 3) == 3)
-          d = u[i].v[k] + v[i].v[k];
-        else if constexpr (GM == 1)
+        if constexpr (GM & 1) {
           d = u[i].v[k];
-        else
+          if constexpr (GM & 8) d = d + q[i].v[k];
+          if constexpr (GM & 2) d = d + v[i].v[k];
+        } else {
           d = v[i].v[k];
+        }
         xh[i].v[k] = ok ? (x - mean) * rstd : 0.f;
         dy[i].v[k] = ok ? d : 0.f;
         dg[i].v[k] = __builtin_fmaf(dy[i].v[k], xh[i].v[k], dg[i].v[k]);
@@ -279,6 +286,8 @@ struct LnArgs {
   const void *a, *b;
   const float *g32;
   const __bf16 *g16;
+  const __bf16 *gx;  // backward: second bf16 gradient of the fp32 output (GM bit 3)
+  long long ldg;     // backward: row stride of g32 (elements)
   const float *gamma, *beta, *mean, *rstd;
   float eps;
   int rows, C;
@@ -300,11 +309,13 @@ template <int CH, int AT, int BT, int GM>
 void ln_bwd_go(const LnArgs &p, int blocks, int rpw) {
   if (p.cs)
     hipLaunchKernelGGL((ln_bwd_kernel<CH, AT, BT, GM, true>), dim3(blocks), dim3(256), 4 * 3 * p.C * sizeof(float),
-                       p.s, p.g32, p.g16, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16, rpw, p.part,
+                       p.s, p.g32, p.g16, p.gx, p.ldg, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16,
+                       rpw, p.part,
                        p.sum16);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<CH, AT, BT, GM, false>), dim3(blocks), dim3(256), 4 * 2 * p.C * sizeof(float),
-                       p.s, p.g32, p.g16, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16, rpw, p.part,
+                       p.s, p.g32, p.g16, p.gx, p.ldg, p.a, p.b, p.gamma, p.mean, p.rstd, p.rows, p.C, p.y32, p.y16,
+                       rpw, p.part,
                        false);
 }
 
@@ -341,8 +352,14 @@ struct LnFwdF {
 template <int CH, int AT, int BT>
 struct LnBwdF {
   static void go(const LnArgs &p, int gm, int blocks, int rpw) {
-    if (gm == 7)
+    if (gm == 11)
+      ln_bwd_go<CH, AT, BT, 11>(p, blocks, rpw);
+    else if (gm == 9)
+      ln_bwd_go<CH, AT, BT, 9>(p, blocks, rpw);
+    else if (gm == 7)
       ln_bwd_go<CH, AT, BT, 7>(p, blocks, rpw);
+    else if (gm == 5)
+      ln_bwd_go<CH, AT, BT, 5>(p, blocks, rpw);
     else if (gm == 3)
       ln_bwd_go<CH, AT, BT, 3>(p, blocks, rpw);
     else if (gm == 1)
@@ -398,6 +415,38 @@ void add_go(const void *a, const void *b, void *out, long long n8, hipStream_t s
   long long g = (n8 + 255) / 256;
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL((add_kernel<AT, BT, OT>), dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, s, a, b, out, n8);
+}
+
+// out rows ldo elements apart, a / b contiguous (rows, C): the refinement stage's two decoder
+// outputs written straight into the halves of their concatenation (SVDFormer.py:86) instead of
+// summed and then copied by torch.cat.  Index arithmetic in 32 bits (n8 < 2^32, host-checked).
+template <int AT, int BT, int OT>
+__global__ __launch_bounds__(256) void add_rows_kernel(const void *__restrict__ a, const void *__restrict__ b,
+                                                       void *__restrict__ out, unsigned n8, unsigned c8,
+                                                       long long ldo) {
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < n8; i += gridDim.x * 256) {
+    const unsigned r = i / c8, c = i - r * c8;
+    V8 x, y;
+    ld8c<AT>(x, a, 8LL * i);
+    ld8c<BT>(y, b, 8LL * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      x.v[k] += y.v[k];
+      if constexpr (AT == 1 && BT == 1) x.v[k] = (float)(__bf16)x.v[k];  // promoted dtype bf16
+    }
+    const long long e = (long long)r * ldo + 8 * c;
+    if constexpr (OT == 0)
+      st8_f32(reinterpret_cast<float *>(out), e, x);
+    else
+      st8_bf16(reinterpret_cast<__bf16 *>(out), e, x);
+  }
+}
+
+template <int AT, int BT, int OT>
+void add_rows_go(const void *a, const void *b, void *out, unsigned n8, unsigned c8, long long ldo, hipStream_t s) {
+  unsigned g = (n8 + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL((add_rows_kernel<AT, BT, OT>), dim3(g < 1 ? 1 : g), dim3(256), 0, s, a, b, out, n8, c8, ldo);
 }
 
 // ---------------------------------------------------------------- path-selection blend
@@ -935,6 +984,31 @@ extern "C" int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype,
   return PCOPS_OK;
 }
 
+extern "C" int pcops_add_rows(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype,
+                              long long rows, int C, long long ld_out, pcops_stream_t stream) {
+  if (rows < 0 || C <= 0 || !dt_ok(a_dtype) || !dt_ok(b_dtype) || !dt_ok(out_dtype)) return PCOPS_ERR_INVALID;
+  if (rows == 0) return PCOPS_OK;
+  if (!a || !b || !out || ld_out < C) return PCOPS_ERR_INVALID;
+  if (C % 8 || ld_out % 8 || rows * (C / 8) >= (1LL << 32)) return PCOPS_ERR_UNSUPPORTED;
+  if ((reinterpret_cast<unsigned long long>(a) | reinterpret_cast<unsigned long long>(b) |
+       reinterpret_cast<unsigned long long>(out)) & 15)
+    return PCOPS_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned n8 = (unsigned)(rows * (C / 8)), c8 = (unsigned)(C / 8);
+  switch (a_dtype * 4 + b_dtype * 2 + out_dtype) {
+    case 0: add_rows_go<0, 0, 0>(a, b, out, n8, c8, ld_out, s); break;
+    case 1: add_rows_go<0, 0, 1>(a, b, out, n8, c8, ld_out, s); break;
+    case 2: add_rows_go<0, 1, 0>(a, b, out, n8, c8, ld_out, s); break;
+    case 3: add_rows_go<0, 1, 1>(a, b, out, n8, c8, ld_out, s); break;
+    case 4: add_rows_go<1, 0, 0>(a, b, out, n8, c8, ld_out, s); break;
+    case 5: add_rows_go<1, 0, 1>(a, b, out, n8, c8, ld_out, s); break;
+    case 6: add_rows_go<1, 1, 0>(a, b, out, n8, c8, ld_out, s); break;
+    default: add_rows_go<1, 1, 1>(a, b, out, n8, c8, ld_out, s); break;
+  }
+  PC_CHECK_LAUNCH();
+  return PCOPS_OK;
+}
+
 namespace {
 unsigned blend_grid(long long n8) {
   long long g = (n8 + 255) / 256;
@@ -1030,7 +1104,7 @@ int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a
                        const float *gamma, const float *mean, const float *rstd, int rows, int C, float *dx32,
                        void *dx16, float *dgamma, float *dbeta, void *dsum, int dsum_src, void *workspace,
                        unsigned long long workspace_bytes, unsigned long long need, hipStream_t s,
-                       bool dy32_bf16 = false) {
+                       bool dy32_bf16 = false, const void *dyx = nullptr, long long ldg = 0) {
   if (rows < 0 || C <= 0) return PCOPS_ERR_INVALID;
   if (C > 512 * kMaxCh || C % 8) return PCOPS_ERR_UNSUPPORTED;
   if (!dgamma || !dbeta) return PCOPS_ERR_INVALID;
@@ -1057,6 +1131,8 @@ int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a
   p.b = b;
   p.g32 = dy32;
   p.g16 = (const __bf16 *)dy16;
+  p.gx = (const __bf16 *)dyx;
+  p.ldg = ldg > 0 ? ldg : C;
   p.gamma = gamma;
   p.mean = mean;
   p.rstd = rstd;
@@ -1069,7 +1145,8 @@ int layernorm_bwd_impl(const float *dy32, const void *dy16, const void *a, int a
   p.sum16 = dsum_src == 1;
   p.s = s;
   ln_dispatch<LnBwdF>(C <= 512 ? 1 : 2, a_dtype, b ? b_dtype : -1, p,
-                      (dy32 ? 1 : 0) | (dy16 ? 2 : 0) | (dy32_bf16 ? 4 : 0), blocks, ln_bwd_rpw(rows));
+                      (dy32 ? 1 : 0) | (dy16 ? 2 : 0) | (dy32_bf16 ? 4 : 0) | (dyx ? 8 : 0), blocks,
+                      ln_bwd_rpw(rows));
   const int np = dsum ? 3 : 2;
   launch_colsum_final(part, blocks, np * C, (void *)dgamma, 0, C, (void *)dbeta, 2 * C, dsum, s, dsum_dt);
   PC_CHECK_LAUNCH();
@@ -1113,6 +1190,21 @@ extern "C" int pcops_layernorm_bwd_bf16g(const void *dy_a, const void *dy16, con
                             dsum ? pcops_layernorm_bwd_colsum_workspace_bytes(rows, C)
                                  : pcops_layernorm_bwd_workspace_bytes(rows, C),
                             (hipStream_t)stream, true);
+}
+
+extern "C" int pcops_layernorm_bwd_ex(const void *dy, int dy_dtype, long long ld_dy, const void *dy_x,
+                                      const void *dy16, const void *a, int a_dtype, const void *b, int b_dtype,
+                                      const float *gamma, const float *mean, const float *rstd, int rows, int C,
+                                      float *dx32, void *dx16, float *dgamma, float *dbeta, void *dsum, int dsum_src,
+                                      void *workspace, unsigned long long workspace_bytes, pcops_stream_t stream) {
+  if (!dy || !dt_ok(dy_dtype)) return PCOPS_ERR_INVALID;
+  if (ld_dy < C || ld_dy % 8 || (reinterpret_cast<unsigned long long>(dy) & 15)) return PCOPS_ERR_INVALID;
+  if (dy_x && dy_dtype != 0) return PCOPS_ERR_UNSUPPORTED;   // instantiated: fp32 dy + dy_x (+ dy16)
+  return layernorm_bwd_impl((const float *)dy, dy16, a, a_dtype, b, b_dtype, gamma, mean, rstd, rows, C, dx32, dx16,
+                            dgamma, dbeta, dsum, dsum_src, workspace, workspace_bytes,
+                            dsum ? pcops_layernorm_bwd_colsum_workspace_bytes(rows, C)
+                                 : pcops_layernorm_bwd_workspace_bytes(rows, C),
+                            (hipStream_t)stream, dy_dtype == 1, dy_x, ld_dy);
 }
 
 extern "C" unsigned long long pcops_colsum_workspace_bytes(long long rows, int C) {

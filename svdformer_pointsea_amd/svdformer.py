@@ -19,8 +19,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import (PosEmbedding, SDG_Decoder, block_sum, cross_attention, linear, self_attention, to_channels,
-                        to_tokens)
+from .attention import (PosEmbedding, SDG_Decoder, block_sum, block_sum_cat, cross_attention, linear, self_attention,
+                        to_channels, to_tokens)
 from .chamfer3D import chamfer_3DDist
 from .model_utils import (SharedFPS, edge_features, fps_subsample, group_local, sample_and_group_knn,
                           sample_and_group_knn_cl)
@@ -499,10 +499,11 @@ class SDG(nn.Module):
 
     @staticmethod
     def _decode(dec, x):
+        """The decoder's output as its last block's (residual, FFN) pair: the concatenation
+        that reads both decoders sums each pair in place (block_sum_cat)."""
         if isinstance(dec, SDG_Decoder):
-            return dec.forward_tokens(x)
-        s, f = dec.forward_tokens(x)
-        return block_sum(s, f, True)
+            return dec.forward_pair(x)
+        return dec.forward_tokens(x)
 
     def forward_tokens(self, local_tok, coarse, f_g, partial):
         """Token-major SDG: local_tok (B,512,C), coarse (B,N,3), f_g (B,512,1),
@@ -524,7 +525,7 @@ class SDG(nn.Module):
         local = _lin(self.mlpp.mlp[2], self.mlpp.mlp[1](_lin(self.mlpp.mlp[0], local_tok)))
         s, f = self.cross1.forward_tokens(F_Q, local)
         F_H_ = self._decode(self.decoder2, block_sum(s, f, True))
-        Tin = torch.cat([F_Q_.to(F_H_.dtype), F_H_], dim=-1)
+        Tin = block_sum_cat(F_Q_, F_H_)   # torch.cat([F_Q_, F_H_]) with each sum written in place
         # (B, C*r, N).reshape(B, C, N*r): point j*N + n takes channels c*r + j of point n.
         r = self.ratio
         if _PS_ROWS:
