@@ -397,7 +397,7 @@ class fork:
     # the only safe way to put hipBLASLt GEMMs inside a forked block)
     enabled = os.environ.get("PCOPS_SIDE_STREAMS", "1") != "0"
 
-    def __init__(self, device, lane=0, inputs=(), base="current", after=None):
+    def __init__(self, device, lane=0, inputs=(), base="current"):
         if base not in ("current", "outer"):
             raise ValueError(f"fork: base must be 'current' or 'outer', not {base!r}")
         self.on = fork.enabled and torch.device(device).type == "cuda"
@@ -412,16 +412,12 @@ class fork:
                     self.on, self.inline = False, True
                     return
             self.main = cur
-            # after: an event recorded earlier on the current stream -- the block starts from that
-            # point instead of the current one (work issued in between runs beside it); under
-            # capture this only changes the order the graph's nodes are created in
-            self.after = after
             self.side = side_stream(device, lane)
             self.inputs = tuple(t for t in inputs if isinstance(t, torch.Tensor) and t.is_cuda)
 
     def __enter__(self):
         if self.on:
-            guarded_wait(self.side, self.main, event=self.after, origin=_origin(self.main))
+            guarded_wait(self.side, self.main, origin=_origin(self.main))
             for t in self.inputs:
                 t.record_stream(self.side)
             self._ctx = torch.cuda.stream(self.side)

@@ -436,11 +436,18 @@ bool bn_fuse(int C) {
   return (!e || atoi(e) != 0) && bn_v(C) * 8 <= 64;
 }
 
-unsigned bn_arrive_slots(int n) {   // host side: `n` consecutive counters no other launch in flight holds
-  static std::atomic<unsigned> next{0};
-  unsigned b = next.fetch_add((unsigned)n) % kBnSlots;
-  if (b + (unsigned)n > kBnSlots) b = 0;
-  return b;
+// host side: `n` consecutive counters no other launch in flight holds.  A captured graph keeps its
+// slots for every replay, so launches made while capturing draw from the lower half and eager launches
+// from the upper half: an eager launch can never share a counter with a replay running beside it
+// (after the eager half wraps it would otherwise be handed a graph's slots).
+unsigned bn_arrive_slots(int n, hipStream_t s) {
+  constexpr unsigned half = kBnSlots / 2;
+  static std::atomic<unsigned> next[2];
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  const bool cap = hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+  unsigned b = next[cap ? 0 : 1].fetch_add((unsigned)n) % half;
+  if (b + (unsigned)n > half) b = 0;
+  return (cap ? 0u : half) + b;
 }
 
 template <int DT, bool FUSE>
@@ -449,7 +456,7 @@ void launch_partial_t(int mode, const void *x, const void *dy, const void *y, co
   const int V = bn_v(C);
   const dim3 grid(chunks, C / 8 / V), block(64 * kBnWaves);
   const size_t lds = FUSE ? (size_t)2 * 16 * V * 8 * sizeof(double) : (size_t)kBnWaves * 2 * V * 8 * sizeof(float);
-  const unsigned slot = FUSE ? bn_arrive_slots(C / 8 / V) : 0u;
+  const unsigned slot = FUSE ? bn_arrive_slots(C / 8 / V, s) : 0u;
   switch (mode) {
     case 0: hipLaunchKernelGGL((bn_partial_kernel<DT, 0, FUSE>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part, fin, slot); break;
     case 1: hipLaunchKernelGGL((bn_partial_kernel<DT, 1, FUSE>), grid, block, lds, s, x, dy, y, mean, rows, C, V, rpc, slope, part, fin, slot); break;

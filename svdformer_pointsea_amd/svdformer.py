@@ -559,7 +559,6 @@ class SDG(nn.Module):
 # A/B, 5 runs each, 51.01-53.04 ms (mean 52.1, bimodal run to run) against 51.64-51.91 (mean 51.78)
 _IMG_STREAM = _os.environ.get("PCOPS_IMG_STREAM", "0") == "1"
 _IMG_FIRST = _os.environ.get("PCOPS_IMG_FIRST", "0") == "1"
-_IMG_EARLY = _os.environ.get("PCOPS_IMG_EARLY", "0") == "1"
 
 
 class _NoFork:
@@ -685,18 +684,10 @@ class Model(nn.Module):
         # PCOPS_IMG_FIRST=1: the image branch issued before the local-encoder fork (A/B of the
         # order the captured graph's nodes are created in)
         f_v = self.encoder.image_features(depth, partial.shape[0]) if _IMG_FIRST else None
-        # PCOPS_IMG_EARLY=1: the image branch issued (captured) before the local encoder, which still
-        # forks from the stream position in front of it -- the same dependencies, the graph's nodes
-        # created image branch first (A/B of the replay's branch start times)
-        after = None
-        if _IMG_EARLY and not _IMG_FIRST and partial.is_cuda:
-            after = torch.cuda.Event()
-            after.record()
-            f_v = self.encoder.image_features(depth, partial.shape[0])
         # the local encoder (EdgeConv kNN, FPS, 1x1-conv GEMMs on rocBLAS: no stream-K)
         # only depends on the partial cloud: it runs on a second HIP stream
         # beside the view/point encoder
-        with fork(partial.device, inputs=(partial_cm, partial), after=after) as br:
+        with fork(partial.device, inputs=(partial_cm, partial)) as br:
             # the partial cloud's FPS, once, first on this stream: the local encoder's and (the
             # first 512 indices) the point encoder's SA module's -- the main stream takes them
             # after the image branch, by an event wait
