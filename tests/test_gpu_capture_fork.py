@@ -202,15 +202,16 @@ def test_model_step_capture_replays(dev, monkeypatch, model_name):
             if r is None:
                 assert p.grad is None
             elif model_name.startswith("pointsea") and name.startswith("encoder.img_feature_extractor."):
-                # PointSea's ResNet-18 is MIOpen's (out of scope).  On the graph's FIRST
-                # launch its stem conv's weight gradient (3 -> 64, 7x7 / 2, MIOpen's wgrad) comes
-                # out 3.3e-4 from eager -- 2.6e-4 of its largest magnitude, the same value on two
-                # boxes, every other parameter within its eager spread -- while replays 2 and 3
-                # match eager (r6 GPU logs; round 5 saw up to 3 % on layers 1-3 before the stem
-                # max-pool moved to libpcops).  Held to 2e-3 of the largest magnitude: a libpcops
-                # fill that does not happen is off by orders of magnitude
+                # PointSea's ResNet-18 is MIOpen's (out of scope).  Its conv weight
+                # gradients differ from eager by up to ~3.5e-3 of their largest magnitude on some
+                # replays, the first or a later one, and not the same layers from run to run
+                # (r6: the stem conv on two boxes; layer3.0.conv1 / layer3.1.conv2 on replays 0 and 1
+                # of another, with the round-5 and the round-6 library alike --
+                # profiles/r6_capture_resnet_flaky.txt).  Held to 4x the eager spread plus 1e-2 of
+                # the largest magnitude: a libpcops fill or dependency that goes missing is off by
+                # orders of magnitude
                 err = float((p.grad - r).abs().max())
-                assert err <= 2e-3 * float(r.abs().max()) + 1e-8, (name, rep, err)
+                assert err <= 4 * float(sp) + 1e-2 * float(r.abs().max()) + 1e-8, (name, rep, err)
             else:
                 # every other parameter on EVERY replay, the first included, within 4x the eager
                 # run-to-run spread of that gradient (MIOpen's conv weight gradients vary by ~1e-3
