@@ -84,9 +84,9 @@ def parse():
                          "the headline (N = 1 only)")
     ap.add_argument("--dry-run-launch", action="store_true",
                     help="with --gpus N > 1 outside torch.distributed.run: print the rank launcher's argv and exit")
-    ap.add_argument("--pmc-attn-json", default=os.path.join(ROOT, "profiles", "r5_pmc_attn.json"),
+    ap.add_argument("--pmc-attn-json", default=os.path.join(ROOT, "profiles", "r6_pmc_attn.json"),
                     help="attention MFMA counters (tools/pmc_attn.py) -> attention.pmc_mfma_util")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r5_pmc_traffic.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r6_pmc_traffic.json"),
                     help="HBM bytes per launch per kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                          "(tools/pmc_traffic.py) -> roofline.traffic")
     ap.add_argument("--pmc-json-pointsea", default=os.path.join(ROOT, "profiles", "r6_pmc_traffic_pointsea.json"),
