@@ -306,6 +306,14 @@ int pcops_transpose_add(const void *a, int a_dtype, const void *b, int b_dtype, 
  * that feeds only GEMMs, models/model_utils.py:616).  16-byte aligned operands. */
 int pcops_add(const void *a, int a_dtype, const void *b, int b_dtype, void *out, int out_dtype, long long n,
               pcops_stream_t stream);
+/* pcops_linear_skinny: y[t][n] = bf16(sum_k x[t][k] A[n][k] (+ bias[n])) for a row-major (rows, K) x,
+ * (N, K) A and (rows, N) y, all bf16 (bias bf16 or NULL), fp32 accumulation on the matrix cores.  The 1x1
+ * convolutions of EdgeConv's first layer (models/model_utils.py:847-881: Conv2d 6 -> 32, 32 -> 32,
+ * 32 -> 64 over B x N x k edge rows, channels_last) -- forward with A = the conv weight, input gradient with
+ * A = its transpose and no bias -- in place of the GEMM library's call.  K in {6, 32, 64}, N in {32, 64};
+ * 16-byte aligned x / y when K % 8 == 0 (8-byte otherwise); A and bias at any bf16 address. */
+int pcops_linear_skinny(const void *x, long long rows, int K, const void *A, const void *bias, void *y, int N,
+                        pcops_stream_t stream);
 /* pcops_add_rows: pcops_add over a contiguous (rows, C) a / b with out's rows ld_out elements apart: the
  * refinement stage's two decoder outputs (SVDFormer.py:79-86, each `s + f` of a block feeding only conv_ps)
  * written straight into the channel halves of `torch.cat([F_Q_, F_H_], 1)` (SVDFormer.py:86), which

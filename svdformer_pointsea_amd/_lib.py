@@ -69,6 +69,7 @@ _SIGS = {
     "pcops_add": (I, [P, I, P, I, P, I, LL, P]),
     "pcops_add_posemb": (I, [P, I, P, P, I, I, I, P, I, P]),
     "pcops_add_rows": (I, [P, I, P, I, P, I, LL, I, LL, P]),
+    "pcops_linear_skinny": (I, [P, LL, I, P, P, P, I, P]),
     "pcops_edge_group": (I, [P, P, I, I, I, I, P, I, P]),
     "pcops_edge_group_grad": (I, [P, I, P, I, I, I, I, P, P]),
     "pcops_max_k": (I, [P, I, LL, I, I, P, P, P]),

@@ -143,6 +143,75 @@ class _Linear(Function):
         return gx, gw, gb, None
 
 
+class _SkinnyLinear(Function):
+    """F.linear for EdgeConv's skinny 1x1 convs under bf16 autocast (Cin in {6, 32, 64}, Cout in {32, 64},
+    ~1 M edge rows): forward and input gradient on pcops_linear_skinny (the weight in registers, one
+    32-row MFMA tile per wave) instead of the GEMM library's 32 x 256 tiles; weight gradient by _wgrad,
+    bias gradient as _Linear's."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, x, w, b, b_dtype=None):
+        K, N = x.shape[-1], w.shape[0]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        w = w.contiguous()
+        y = torch.empty(x2.shape[0], N, dtype=torch.bfloat16, device=x.device)
+        with torch.cuda.device(x.device):
+            call("linear_skinny", lib().pcops_linear_skinny, ptr(x2), x2.shape[0], K, ptr(w),
+                 ptr(None if b is None else b.contiguous()), ptr(y), N, stream_of(x))
+        ctx.save_for_backward(x2, w)
+        ctx.has_b, ctx.b_dtype, ctx.xshape = b is not None, b_dtype, x.shape
+        ctx.side = _lib.on_side_stream()
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, g):
+        x2, w = ctx.saved_tensors
+        N, K = w.shape
+        g2 = g.reshape(-1, N)
+        if not g2.is_contiguous() or g2.dtype != torch.bfloat16:
+            g2 = g2.contiguous().to(torch.bfloat16)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            if N in (32, 64) and K in (32, 64):
+                gx = torch.empty(g2.shape[0], K, dtype=torch.bfloat16, device=g2.device)
+                with torch.cuda.device(g2.device):
+                    call("linear_skinny", lib().pcops_linear_skinny, ptr(g2), g2.shape[0], N, ptr(w.t().contiguous()),
+                         ptr(None), ptr(gx), K, stream_of(g2))
+            else:
+                with _lib.no_stream_k() if ctx.side else _nullctx():
+                    gx = g2 @ w
+            gx = gx.view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            with _lib.no_stream_k() if ctx.side else _nullctx():
+                gw = _wgrad(g2, x2, w.dtype)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            pre = _take_sum(g)
+            gb = pre if pre is not None else colsum(g2, out_dtype=ctx.b_dtype)
+            if ctx.b_dtype is not None and gb.dtype != ctx.b_dtype:
+                gb = gb.to(ctx.b_dtype)
+        return gx, gw, gb, None
+
+
+# A/B switch (default off): EdgeConv's skinny 1x1 convs on pcops_linear_skinny.  Their kernels are 2-6x faster
+# than the side stream's rocBLAS GEMMs (gcn_1 forward 395 -> 136 us, the input gradients too), but the local
+# encoder runs beside the critical path in both models: PCN 47.93-48.03 -> 48.09-48.33 ms, PointSea 30.49 ->
+# 30.53 ms (profiles/r6_skinny_ab.txt) -- no step gain, so the GEMM library path stays the default
+_SKINNY = os.environ.get("PCOPS_SKINNY", "0") == "1"
+
+
+def linear_skinny(x, w, b=None):
+    """_SkinnyLinear when x / w fit it (bf16 autocast, CUDA, K in {6, 32, 64}, N in {32, 64}), else None."""
+    if not (_SKINNY and x.is_cuda and _want_bf16() and x.shape[-1] in (6, 32, 64) and w.shape[0] in (32, 64)
+            and w.dim() == 2 and w.shape[1] == x.shape[-1] and x.dtype == torch.bfloat16
+            and x.data_ptr() % (16 if x.shape[-1] % 8 == 0 else 8) == 0):
+        return None
+    return _SkinnyLinear.apply(x, w, b, _bdt(b))
+
+
 _PRESUM = "_pcops_bias_colsum"   # attribute a gradient tensor carries when its column sum is known
 
 

@@ -19,8 +19,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .attention import (PosEmbedding, SDG_Decoder, block_sum, block_sum_cat, cross_attention, linear, self_attention,
-                        to_channels, to_tokens)
+from .attention import (PosEmbedding, SDG_Decoder, block_sum, block_sum_cat, cross_attention, linear, linear_skinny,
+                        self_attention, to_channels, to_tokens)
 from .chamfer3D import chamfer_3DDist
 from .model_utils import (SharedFPS, edge_features, fps_subsample, group_local, sample_and_group_knn,
                           sample_and_group_knn_cl)
@@ -121,7 +121,10 @@ def conv1x1(x, conv, where="sa"):
     is channels_last again.  Other convs go to MIOpen unchanged."""
     if (_CONV1X1 in ("all", where) and x.is_cuda and x.dim() == 4 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
             and conv.padding == (0, 0) and conv.groups == 1 and x.is_contiguous(memory_format=torch.channels_last)):
-        y = linear(x.permute(0, 2, 3, 1), conv.weight.view(conv.out_channels, -1), conv.bias)
+        xt, w = x.permute(0, 2, 3, 1), conv.weight.view(conv.out_channels, -1)
+        y = linear_skinny(xt, w, conv.bias) if where == "edge" else None
+        if y is None:
+            y = linear(xt, w, conv.bias)
         return y.permute(0, 3, 1, 2)
     return conv(x)
 
