@@ -184,14 +184,16 @@ def test_pos_grad_mailbox_bitwise(dev, monkeypatch, kind, L, C):
         assert torch.equal(u, v)
 
 
-def test_sdg_refine_glue_bitwise(dev, monkeypatch):
-    """The PCN refinement stage (SDG, SVDFormer.py:38-104, ratio 4) with both changes on against both off:
-    output and every gradient bitwise."""
+@pytest.mark.parametrize("dataset", ["PCN", "ShapeNet"])
+def test_sdg_refine_glue_bitwise(dev, monkeypatch, dataset):
+    """The refinement stage (SDG, SVDFormer.py:38-104) with both changes on against both off: output and
+    every gradient bitwise -- with self_attention decoders ("PCN") and with SDG_Decoder (the bench
+    model's PCNConfig, TEST_DATASET "ShapeNet": its sa2 pair reaches the concatenation)."""
     import svdformer_pointsea_amd.attention as A
     from svdformer_pointsea_amd.svdformer import SDG
 
     torch.manual_seed(5)
-    sdg = SDG(ratio=2, hidden_dim=512, dataset="PCN").to(dev)
+    sdg = SDG(ratio=2, hidden_dim=512, dataset=dataset).to(dev)
     B, N = 2, 256
     local0 = torch.randn(B, 512, 256, device=dev) * 0.1
     coarse0 = torch.rand(B, N, 3, device=dev)
