@@ -196,6 +196,15 @@ def kernel_work(name, a):
         adt, has_b, bdt, rows, C = a[1], a[2] is not None, a[3], a[7], a[8]
         per = (4 if adt == 0 else 2) + ((4 if bdt == 0 else 2) if has_b else 0) + 6
         return float(per) * rows * C, "GB/s", HBM_PEAK, "hbm"
+    if name == "layernorm_bwd" and len(a) == 23:
+        # pcops_layernorm_bwd_ex: dy, dyt, ld, dy_x, dy16, a, adt, b, bdt, gamma, mean, rstd, rows, C, dx32, dx16, ...
+        # read a (+ b), dy (+ dy_x) (+ dy16), write dx32 / dx16 as present
+        dyt, has_x, has_16, adt, has_b, bdt, rows, C = a[1], a[3] is not None, a[4] is not None, a[6], \
+            a[7] is not None, a[8], a[12], a[13]
+        per = ((4 if adt == 0 else 2) + ((4 if bdt == 0 else 2) if has_b else 0) + (4 if dyt == 0 else 2)
+               + (2 if has_x else 0) + (2 if has_16 else 0) + (4 if a[14] is not None else 0)
+               + (2 if a[15] is not None else 0))
+        return float(per) * rows * C, "GB/s", HBM_PEAK, "hbm"
     if name == "layernorm_bwd":
         adt, has_b, bdt, rows, C = a[3], a[4] is not None, a[5], a[9], a[10]
         per = (4 if adt == 0 else 2) + ((4 if bdt == 0 else 2) if has_b else 0) + 6 + 4 + 2
@@ -273,6 +282,10 @@ def kernel_work(name, a):
         return float(a[4] * (es(a[1]) + 8 + es(a[6]))), "GB/s", HBM_PEAK, "hbm"
     if name == "blend_bwd":      # g, gdt, score, sdt, a, b, n, da, db, ds: read g, score, a, b; write da, db, ds
         return float(a[6] * (es(a[1]) + 2 * es(a[3]) + 16)), "GB/s", HBM_PEAK, "hbm"
+    if name == "add_rows":       # a, adt, b, bdt, out, odt, rows, C, ld_out: read a + b, write out's rows
+        return float(a[6] * a[7] * (es(a[1]) + es(a[3]) + es(a[5]))), "GB/s", HBM_PEAK, "hbm"
+    if name == "linear_skinny":  # x, rows, K, A, bias, y, N: read x, write y (bf16; the weight stays on chip)
+        return float(2 * a[1] * (a[2] + a[6])), "GB/s", HBM_PEAK, "hbm"
     if name == "add_posemb":     # a, adt, cd, div, B, N, H, out, odt: read a + cd, write out
         return float(a[4] * a[5] * (a[6] * (es(a[1]) + es(a[8])) + 4)), "GB/s", HBM_PEAK, "hbm"
     if name == "max_k":          # x, dt, rows, K, C, out, arg: read K rows, write the max + a uint8 argmax

@@ -123,3 +123,23 @@ def test_oversized_line_drops_optional_fields():
     full["fps_us_per_round"] = {f"k{i}": 1.0 for i in range(2000)}   # a runaway optional field
     line = bench.compact(full)
     assert len(line.encode()) < 8192 and "roofline" in json.loads(line)
+
+
+def test_layernorm_bwd_work_models_both_layouts():
+    """The LayerNorm backward's byte model reads the argument layout of the entry point that ran: the
+    round-6 pcops_layernorm_bwd_ex (23 args, dy first with its dtype, stride and the extra gradient) and
+    the older pcops_layernorm_bwd(_colsum / _bf16g) -- a mis-read layout priced the round-6 line at 2e20
+    times the HBM peak."""
+    import bench
+
+    rows, C = 65536, 512
+    ex = (1, 1, 1024, None, 2, 3, 0, 4, 1, 5, 6, 7, rows, C, 8, 9, 10, 11, 12, 3, 13, 1 << 20, 14)
+    old = (1, 2, 3, 0, 4, 1, 5, 6, 7, rows, C, 8, 9, 10, 11, 13, 1 << 20, 14)
+    for a in (ex, old):
+        work, unit, peak, bound = bench.kernel_work("layernorm_bwd", a)
+        assert unit == "GB/s" and bound == "hbm"
+        assert 8 * rows * C <= work <= 24 * rows * C, work
+    # ex: fp32 a + bf16 b + bf16 dy (strided) + bf16 dy16 + fp32 dx32 + bf16 dx16 = 16 B per element
+    assert bench.kernel_work("layernorm_bwd", ex)[0] == 16.0 * rows * C
+    assert bench.kernel_work("add_rows", (1, 0, 2, 1, 3, 1, rows, C, 2 * C, 4))[0] == 8.0 * rows * C
+    assert bench.kernel_work("linear_skinny", (1, rows, 6, 2, 3, 4, 32, 5))[0] == 2.0 * rows * 38
