@@ -171,6 +171,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a,
 // of waves atomically adding into the same 2C floats serialise), then summed
 // by colsum_final_kernel in a fixed order.
 int ln_bwd_rpw(int rows) {
+  static const int forced = [] {   // PCOPS_LN_RPW: rows per wave forced (A/B runs)
+    const char *e = getenv("PCOPS_LN_RPW");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) return forced;
   const int r = (rows + 8191) / 8192;
   return r < 4 ? 4 : (r > 16 ? 16 : r);
 }
