@@ -101,6 +101,38 @@ __device__ __forceinline__ void st8_bf16(__bf16 *p, long long e, const V8 &o) {
   *reinterpret_cast<bf16x8_t *>(p + e) = x;
 }
 
+// 8 elements as raw 16-byte vectors (fp32: two, bf16: one), converted at their use by cvt8 (the values of
+// ld8c): the LayerNorm backward holds a row's bf16 operands packed, 4 registers per 8 elements, instead of 8
+template <int DT>
+struct Raw8;
+template <>
+struct Raw8<0> {
+  float4 x, y;
+};
+template <>
+struct Raw8<1> {
+  uint4 x;
+};
+template <int DT>
+__device__ __forceinline__ void ldraw(Raw8<DT> &r, const void *p, long long e) {
+  if constexpr (DT == 0) {
+    r.x = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + e);
+    r.y = *reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(p) + e + 4);
+  } else {
+    r.x = *reinterpret_cast<const uint4 *>(reinterpret_cast<const __bf16 *>(p) + e);
+  }
+}
+template <int DT>
+__device__ __forceinline__ float raw_at(const Raw8<DT> &r, int k) {
+  if constexpr (DT == 0) {
+    const float v[8] = {r.x.x, r.x.y, r.x.z, r.x.w, r.y.x, r.y.y, r.y.z, r.y.w};
+    return v[k];
+  } else {
+    const unsigned w = k < 2 ? r.x.x : k < 4 ? r.x.y : k < 6 ? r.x.z : r.x.w;
+    return __uint_as_float((k & 1) ? (w & 0xffff0000u) : (w << 16));   // bf16 -> fp32 is a shift
+  }
+}
+
 // AT: a's dtype; BT: b's dtype or -1 (no residual)
 template <int CH, int AT, int BT>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a, const void *__restrict__ b,
@@ -170,6 +202,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void *__restrict__ a,
 // written once per block to a [blocks][2C] scratch (plain stores -- thousands
 // of waves atomically adding into the same 2C floats serialise), then summed
 // by colsum_final_kernel in a fixed order.
+#ifndef PCOPS_LN_RAW
+#define PCOPS_LN_RAW 1   // LayerNorm backward: bf16 operands held packed until used (A/B builds: 0)
+#endif
+
 int ln_bwd_rpw(int rows) {
   static const int forced = [] {   // PCOPS_LN_RPW: rows per wave forced (A/B runs)
     const char *e = getenv("PCOPS_LN_RPW");
@@ -216,7 +252,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
     const float mean = mean_in[row], rstd = rstd_in[row];
     // all loads of the row first (clamped chunk index, no branches), then the
     // arithmetic; lanes past the row end carry dy = xh = 0
-    V8 xh[CH], dy[CH], t[CH], u[CH], v[CH], q[(GM & 8) ? CH : 1];
+    V8 xh[CH], dy[CH];
+#if PCOPS_LN_RAW
+    // the row's operands as loaded, bf16 ones packed (converted where used: a shift per value)
+    Raw8<AT> ra[CH];
+    Raw8<BT < 0 ? 1 : BT> rb[CH];
+    Raw8<(GM & 4) ? 1 : 0> ru[CH];
+    Raw8<1> rq[(GM & 8) ? CH : 1], rv[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int c8 = 8 * min(lane + 64 * i, nch - 1);
+      const long long e = base + c8;
+      ldraw<AT>(ra[i], a, e);
+      if constexpr (BT >= 0) ldraw<BT>(rb[i], b, e);
+      if constexpr (GM & 1) ldraw<(GM & 4) ? 1 : 0>(ru[i], g32, (long long)row * ldg + c8);
+      if constexpr (GM & 8) ldraw<1>(rq[i], gx, e);
+      if constexpr (GM & 2) ldraw<1>(rv[i], g16, e);
+    }
+#else
+    V8 t[CH], u[CH], v[CH], q[(GM & 8) ? CH : 1];
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int c8 = 8 * min(lane + 64 * i, nch - 1);
@@ -227,12 +281,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
       if constexpr (GM & 8) ld8c<1>(q[i], gx, e);
       if constexpr (GM & 2) ld8c<1>(v[i], g16, e);
     }
+#endif
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const bool ok = lane + 64 * i < nch;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
+#if PCOPS_LN_RAW
+        float x = raw_at<AT>(ra[i], k);
+        if constexpr (BT >= 0) x += raw_at<BT < 0 ? 1 : BT>(rb[i], k);
+        float d;
+        if constexpr (GM & 1) {
+          d = raw_at<(GM & 4) ? 1 : 0>(ru[i], k);
+          if constexpr (GM & 8) d = d + raw_at<1>(rq[i], k);
+          if constexpr (GM & 2) d = d + raw_at<1>(rv[i], k);
+        } else {
+          d = raw_at<1>(rv[i], k);
+        }
+#else
         float x = xh[i].v[k];
         if constexpr (BT >= 0) x += t[i].v[k];
         float d;
@@ -243,6 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CH == 1 ? 4
         } else {
           d = v[i].v[k];
         }
+#endif
         xh[i].v[k] = ok ? (x - mean) * rstd : 0.f;
         dy[i].v[k] = ok ? d : 0.f;
         dg[i].v[k] = __builtin_fmaf(dy[i].v[k], xh[i].v[k], dg[i].v[k]);
