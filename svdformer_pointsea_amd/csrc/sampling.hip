@@ -544,6 +544,26 @@ int fps_split_ppt() {  // PCOPS_FPS_SPLIT_PPT: points per reference thread above
   return v;
 }
 
+// One FPS workgroup per CU.  An FPS launch is B workgroups (one per cloud), each a serial chain of M rounds
+// bound by its own CU's VALU and LDS latency; the workgroup dispatcher may place two of them -- of one launch,
+// or of the FPS launches the models run side by side on other streams (the loss's gt chain, the next step's
+// crop, the partial cloud) -- on the same CU, where they split that CU's issue slots and each runs up to 2x
+// slower.  Every FPS launch therefore reserves kFpsExclLds bytes of dynamic LDS it never touches: two FPS
+// workgroups (> 80 KB each) cannot share a CU's 160 KB.  PCOPS_FPS_EXCL=0 turns the reservation off (A/B).
+constexpr int kFpsExclLds = 96 * 1024;
+template <auto K>
+unsigned fps_excl_lds() {
+  static const unsigned bytes = [] {
+    const char *e = getenv("PCOPS_FPS_EXCL");
+    if (e && e[0] == '0') return 0u;
+    return hipFuncSetAttribute((const void *)K, hipFuncAttributeMaxDynamicSharedMemorySize, kFpsExclLds) ==
+                   hipSuccess
+               ? (unsigned)kFpsExclLds
+               : 0u;
+  }();
+  return bytes;
+}
+
 unsigned grid_for(size_t total, int block) {
   size_t g = (total + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -583,7 +603,8 @@ int fps_impl(const float *xyz, const int *counts, int B, int N, int M, int *idx,
     const int ppl = R * ppt;
 #define FPS_WAVE_CASE(P)                                                                                     \
   if (ppl <= P) {                                                                                            \
-    hipLaunchKernelGGL((fps_wave_kernel<P>), dim3(B), dim3(64), 0, s, xyz, N, M, T, L, R, ppt, idx, counts); \
+    hipLaunchKernelGGL((fps_wave_kernel<P>), dim3(B), dim3(64), fps_excl_lds<fps_wave_kernel<P>>(), s, xyz, N, \
+                       M, T, L, R, ppt, idx, counts);                                                        \
     PC_CHECK_LAUNCH();                                                                                       \
     return PCOPS_OK;                                                                                         \
   }
@@ -607,7 +628,8 @@ int fps_impl(const float *xyz, const int *counts, int B, int N, int M, int *idx,
       const int ppl = R * ppt;
 #define FPS_MW_CASE(P)                                                                                        \
   if (ppl <= P) {                                                                                             \
-    hipLaunchKernelGGL((fps_mw_kernel<P, NW>), dim3(B), dim3(64 * NW), 0, s, xyz, N, M, T, L, R, ppt, idx,   \
+    const unsigned lds_ = fps_excl_lds<fps_mw_kernel<P, NW>>();                                              \
+    hipLaunchKernelGGL((fps_mw_kernel<P, NW>), dim3(B), dim3(64 * NW), lds_, s, xyz, N, M, T, L, R, ppt, idx, \
                        counts);                                                                               \
     PC_CHECK_LAUNCH();                                                                                        \
     return PCOPS_OK;                                                                                          \
@@ -627,8 +649,11 @@ int fps_impl(const float *xyz, const int *counts, int B, int N, int M, int *idx,
     const int per = (ppt + split - 1) / split;
     const int nwt = nthreads / 64;
 #define FPS_LAUNCH(P, AR, CN)                                                                             \
-  hipLaunchKernelGGL((fps_reg_kernel<P, AR, CN>), dim3(B), dim3(nthreads * split), 0, s, xyz, N, M, T, L, nwt, \
-                     split, idx, counts)
+  do {                                                                                                    \
+    const unsigned lds_ = fps_excl_lds<fps_reg_kernel<P, AR, CN>>();                                      \
+    hipLaunchKernelGGL((fps_reg_kernel<P, AR, CN>), dim3(B), dim3(nthreads * split), lds_, s, xyz, N, M, T, L, \
+                       nwt, split, idx, counts);                                                          \
+  } while (0)
 #define FPS_CASE(P)                                                                                       \
   if (per <= P) {                                                                                         \
     const bool ar = !(fps_v1() || nthreads * split > 512);                                                \
@@ -654,8 +679,8 @@ int fps_impl(const float *xyz, const int *counts, int B, int N, int M, int *idx,
 #undef FPS_LAUNCH
   }
   if (!workspace || workspace_bytes < pcops_fps_workspace_bytes(B, N)) return PCOPS_ERR_WORKSPACE;
-  hipLaunchKernelGGL(fps_stream_kernel, dim3(B), dim3(nthreads), 0, s, xyz, N, M, T, L, (float *)workspace, idx,
-                     counts);
+  hipLaunchKernelGGL(fps_stream_kernel, dim3(B), dim3(nthreads), fps_excl_lds<fps_stream_kernel>(), s, xyz, N, M, T,
+                     L, (float *)workspace, idx, counts);
   PC_CHECK_LAUNCH();
   return PCOPS_OK;
 }
