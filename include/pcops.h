@@ -58,6 +58,14 @@ int pcops_furthest_point_sampling(const float *xyz, int B, int N, int M, int *id
 int pcops_furthest_point_sampling_counts(const float *xyz, const int *counts, int B, int N, int M, int *idx,
                                          void *workspace, unsigned long long workspace_bytes,
                                          pcops_stream_t stream);
+/* seprate_point_cloud's crop (utils/helpers.py:96-111: torch.argsort of the distances to the crop centre,
+ * then idx[num_crop:] / idx[:num_crop] of each sample), batched: dist (B,N) fp32, xyz (B,N,3) fp32; the
+ * points of cloud b ordered by distance ascending (ties by point index, NaN last), ranks
+ * start[b] .. start[b] + count[b] - 1 written to rows 0.. of out (B,n_max,3), rows j >= count[b] hold
+ * the rank-(start[b]+j, clamped to N-1) point times 0; counts (B) int32 <- count[b] (may be NULL).
+ * start / count int64 (B) on the device; count NULL means N - start[b].  N <= 16384. */
+int pcops_crop_pack(const float *dist, const float *xyz, const long long *start, const long long *count, int B, int N,
+                    int n_max, float *out, int *counts, pcops_stream_t stream);
 
 /* gather_points(points, idx): sampling.cpp:15-38, sampling_gpu.cu:8-30.
  * points (B,C,N), idx (B,M) -> out (B,C,M). */

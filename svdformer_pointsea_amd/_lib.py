@@ -68,6 +68,7 @@ _SIGS = {
     "pcops_transpose_add": (I, [P, I, P, I, P, I, P, I, I, I, I, P]),
     "pcops_add": (I, [P, I, P, I, P, I, LL, P]),
     "pcops_add_posemb": (I, [P, I, P, P, I, I, I, P, I, P]),
+    "pcops_crop_pack": (I, [P, P, P, P, I, I, I, P, P, P]),
     "pcops_add_rows": (I, [P, I, P, I, P, I, LL, I, LL, P]),
     "pcops_linear_skinny": (I, [P, LL, I, P, P, P, I, P]),
     "pcops_edge_group": (I, [P, P, I, I, I, I, P, I, P]),
