@@ -12,7 +12,7 @@ dev = torch.device("cuda", 0)
 g = torch.Generator(device="cpu").manual_seed(0)
 tag = "wave=" + os.environ.get("PCOPS_FPS_WAVE", "8") + " mw=" + os.environ.get("PCOPS_FPS_MW", "0")
 for B, N, M, kind in [(32, 16384, 2048, "gauss"), (32, 16384, 2048, "surface"), (16, 8192, 2048, "surface"),
-                      (32, 2304, 512, "surface"), (32, 4096, 1024, "gauss"), (32, 2048, 512, "gauss"),
+                      (32, 2304, 512, "surface"), (16, 2304, 1024, "surface"), (32, 4096, 1024, "gauss"), (32, 2048, 512, "gauss"),
                       (32, 2048, 256, "gauss"), (32, 512, 128, "gauss"), (32, 1024, 256, "gauss")]:
     x = torch.randn(B, N, 3, generator=g)
     if kind == "surface":  # points on ellipsoid surfaces, like the PCN / ShapeNet gt clouds
